@@ -1,0 +1,178 @@
+/*
+ * flacgpu.h -- C ABI of libflacgpu.so, the MI355X (gfx950) FLAC block encoder.
+ *
+ * Drop-in boundary for toastori/zig-flac's per-block encode path
+ * (reference: src/lib.zig re-exports; the hot call is Encoder.writeFrame,
+ * src/lib/encoder.zig:234-284).  Plain pointers and sizes only; no torch or
+ * HIP types in any signature except the opaque `void *hip_stream` of the
+ * device-resident entry points.  Each entry point cites the reference
+ * interface it replaces.  The Zig `extern` declarations a maintainer adds to
+ * the reference are in INTEGRATION.md.
+ *
+ * Output bytes are identical to the reference encoder's for the same input
+ * (see DESIGN.md for the parity evidence and the one documented divergence,
+ * a reference undefined-behaviour case).
+ *
+ * Threading: one context per GPU per host thread; a context is not
+ * thread-safe.  All functions return FLACGPU_OK (0) or a negative error code.
+ */
+#ifndef FLACGPU_H
+#define FLACGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLACGPU_ABI_VERSION 1
+
+/* Error codes (map to the Zig error set
+ * {OutOfMemory, WriteFailed, DeviceError, InvalidConfig, InvalidInput}). */
+enum {
+    FLACGPU_OK = 0,
+    FLACGPU_ERR_INVALID_CONFIG = -1, /* Config outside what the reference accepts */
+    FLACGPU_ERR_INVALID_INPUT = -2,  /* bad pointer / size / alignment */
+    FLACGPU_ERR_OUT_OF_MEMORY = -3,  /* Allocator.Error.OutOfMemory (encoder.zig:48) */
+    FLACGPU_ERR_OUTPUT_TOO_SMALL = -4, /* Writer.Error.WriteFailed analogue */
+    FLACGPU_ERR_DEVICE = -5,         /* HIP runtime failure or no gfx950 device */
+    FLACGPU_ERR_INTERNAL = -6        /* device-side invariant violated */
+};
+
+/* Encoder.Config + Config.Feature (encoder.zig:609-656) and the per-frame
+ * FrameInfo fields that are constant over a stream (encoder.zig:658-663). */
+typedef struct {
+    uint32_t sample_rate;          /* FrameInfo.sample_rate (u20) */
+    uint16_t block_size;           /* Config.block_size: 1..4096 (default 4096, encoder.zig:644) */
+    uint8_t channels;              /* 1..8 */
+    uint8_t bits_per_sample;       /* 8, 16, 24 or 32 (frame_writer.zig:221-233) */
+    uint8_t stereo_decorrelation;  /* Feature.stereo_decorrelation (default 1) */
+    uint8_t max_rice_part_order;   /* Feature.max_rice_order, 0..8 (default 8) */
+    uint8_t max_rice_param;        /* Feature.max_rice_param, 1..30 (default 30) */
+    uint8_t prediction;            /* Feature.prediction: 0 = fixed (the only value the
+                                      reference implements; it never reads the field) */
+} flacgpu_config;
+
+/* Config.default(channels, bit_depth) (encoder.zig:642-655). */
+flacgpu_config flacgpu_config_default(uint32_t channels, uint32_t bits_per_sample, uint32_t sample_rate);
+
+typedef struct flacgpu_ctx flacgpu_ctx;
+
+/* Encoder.init (encoder.zig:44-118): allocates all device scratch up front
+ * for up to `max_frames_per_call` frames per call (0 = 32768).  device is the
+ * HIP ordinal. */
+int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_call, flacgpu_ctx **out);
+/* Encoder.deinit (encoder.zig:121-164). */
+void flacgpu_close(flacgpu_ctx *ctx);
+
+const char *flacgpu_strerror(int code);
+int flacgpu_abi_version(void);
+
+/* maxFrameBytes (encoder.zig:583-595) of the reference, and the tight bound
+ * the GPU path uses for its per-frame slots. */
+size_t flacgpu_reference_max_frame_bytes(const flacgpu_config *cfg);
+size_t flacgpu_frame_bound_bytes(const flacgpu_config *cfg);
+
+/* ---- Host-buffer entry points (synchronous) ---------------------------- */
+
+/* Batched Encoder.writeFrame (encoder.zig:234) driven the way wav2flac.encode
+ * drives it (wav2flac.zig:66-97): `pcm` holds n_samples interleaved
+ * little-endian samples of bytes_per_sample (= bits/8) bytes, exactly as a WAV
+ * data chunk stores them (WavReader.fillSamples, wav_reader.zig:44-91).  Frames
+ * of cfg.block_size samples are numbered from first_frame_number; the last
+ * one may be short.  Writes the concatenated frames to out[0..*out_len) and
+ * the per-frame byte counts (the u24 writeFrame returns) to frame_bytes[],
+ * in frame order.  As in the reference, the caller drives the MD5
+ * separately (flacgpu_md5_update with the same bytes). */
+int flacgpu_encode_frames(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
+                          uint64_t first_frame_number, uint8_t *out, size_t out_cap, size_t *out_len,
+                          uint32_t *frame_bytes);
+
+/* Encoder.writeFrame for one frame, exactly the reference call: the caller
+ * provides planar i32 samples (the reference's Encoder.samples[ch][0..n],
+ * encoder.zig:23, each within bits_per_sample signed range), the frame number
+ * (u36) and n = FrameInfo.samples_count (1..block_size).  Writes the frame to
+ * out and its size to *frame_bytes. */
+int flacgpu_encode_frame_planar(flacgpu_ctx *ctx, const int32_t *const planes[8], uint32_t n,
+                                uint64_t frame_number, uint8_t *out, size_t out_cap, uint32_t *frame_bytes);
+
+/* ---- Streaming MD5 (md5.zig, fed by wav_reader.zig:66; finalised by
+ *      Encoder.finalizeStreamInfoMd5, encoder.zig:168-170) on the GPU ------- */
+int flacgpu_md5_init(flacgpu_ctx *ctx);
+int flacgpu_md5_update(flacgpu_ctx *ctx, const void *data, size_t len);
+int flacgpu_md5_final(flacgpu_ctx *ctx, uint8_t digest[16]);
+
+/* ---- Device-resident entry points (asynchronous on hip_stream) --------- */
+
+/* A plan describes a batch of independent streams (files) laid out in one
+ * device PCM buffer: stream s holds stream_samples[s] interleaved samples
+ * starting at byte offset stream_offsets[s] (4-byte aligned).  Frames of
+ * every stream are numbered from 0.  The plan precomputes the frame table
+ * (device memory) so repeated calls launch no host work. */
+typedef struct flacgpu_plan flacgpu_plan;
+int flacgpu_plan_create(flacgpu_ctx *ctx, uint32_t n_streams, const uint64_t *stream_offsets,
+                        const uint64_t *stream_samples, uint32_t bytes_per_sample, flacgpu_plan **out);
+void flacgpu_plan_destroy(flacgpu_plan *plan);
+uint64_t flacgpu_plan_frames(const flacgpu_plan *plan);
+/* Bytes of device output capacity the plan may need (sum of frame bounds). */
+uint64_t flacgpu_plan_out_bound(const flacgpu_plan *plan);
+/* First frame index of stream s inside the plan's frame table. */
+uint64_t flacgpu_plan_stream_first_frame(const flacgpu_plan *plan, uint32_t s);
+
+/* Encode every frame of the plan from device PCM d_pcm into the compacted
+ * device buffer d_out (capacity out_cap).  Per frame: d_frame_bytes[f] (u32)
+ * and d_frame_offsets[f] (u64 byte offset of frame f in d_out; stream s's
+ * bitstream is the contiguous range starting at its first frame's offset).
+ * d_total (u64) receives the total byte count.  If d_md5 is non-NULL, the MD5
+ * of every stream's raw PCM bytes is computed on the GPU into d_md5[16*s].
+ * Nothing is synchronised; all work is queued on hip_stream (NULL = the
+ * context's own stream). */
+int flacgpu_encode_plan_device(flacgpu_ctx *ctx, const flacgpu_plan *plan, const void *d_pcm, uint8_t *d_out,
+                               uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets,
+                               uint64_t *d_total, uint8_t *d_md5, void *hip_stream);
+
+/* ---- Instrumentation ---------------------------------------------------- */
+/* Kernel ids for flacgpu_kernel_time. */
+enum { FLACGPU_K_ENCODE = 0, FLACGPU_K_ENCODE_TAIL = 1, FLACGPU_K_SCAN = 2, FLACGPU_K_COMPACT = 3, FLACGPU_K_MD5 = 4,
+       FLACGPU_K_COUNT = 5 };
+/* When enabled, every launch of kernel k is bracketed by HIP events on the
+ * stream it runs on; flacgpu_kernel_time returns the number of timed launches
+ * and their summed device milliseconds since the last reset. */
+int flacgpu_set_timing(flacgpu_ctx *ctx, int enable);
+int flacgpu_kernel_time(flacgpu_ctx *ctx, int kernel, uint64_t *launches, double *total_ms);
+int flacgpu_reset_timing(flacgpu_ctx *ctx);
+
+/* Decision records (for parity tests): when enabled, each encode call also
+ * stores one flacgpu_frame_record per frame, readable with
+ * flacgpu_get_records after a synchronous call. */
+typedef struct {
+    uint8_t type;       /* 0 CONSTANT, 1 VERBATIM, 2 FIXED */
+    uint8_t waste;
+    uint8_t bits;       /* channel bit depth before waste removal */
+    uint8_t order;
+    uint8_t part_order;
+    uint8_t method;     /* 0 FOUR, 1 FIVE */
+    uint8_t written;    /* 1 if this candidate is in the bitstream */
+    uint8_t pad;
+    uint32_t pad2;
+    uint64_t estimate;
+    int64_t constant;
+    uint8_t params[256];
+} flacgpu_subframe_record;
+
+typedef struct {
+    uint32_t channel_code;
+    uint32_t n_cand;
+    uint32_t frame_bytes;
+    uint32_t pad;
+    flacgpu_subframe_record cand[8];
+} flacgpu_frame_record;
+
+int flacgpu_set_records(flacgpu_ctx *ctx, int enable);
+int flacgpu_get_records(flacgpu_ctx *ctx, flacgpu_frame_record *out, uint64_t max_frames, uint64_t *n_frames);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

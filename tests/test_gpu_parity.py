@@ -1,0 +1,178 @@
+"""GPU (libflacgpu.so on gfx950) vs the CPU restatement: bit-exact frames.
+
+Every test calls through the C ABI and compares with oracle/ on the same
+seeded input: whole-stream bytes, per-frame sizes, per-candidate decision
+records, and a round trip through the independent verifier decoder.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle_ref
+import synth
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [
+    # channels, bits, rate
+    (2, 16, 44100),
+    (2, 24, 96000),
+    (2, 32, 192000),
+    (1, 16, 44100),
+    (8, 24, 96000),
+    (3, 16, 48000),
+    (2, 8, 8000),
+    (1, 24, 96000),
+    (1, 32, 48000),
+]
+
+_encoders = {}
+
+
+def gpu_encoder(ch, bits, rate, **kw):
+    import flacgpu
+
+    key = (ch, bits, rate, tuple(sorted(kw.items())))
+    if key not in _encoders:
+        _encoders[key] = flacgpu.Encoder(ch, bits, rate, max_frames=1024, **kw)
+    return _encoders[key]
+
+
+def _diff_msg(a: bytes, b: bytes) -> str:
+    n = min(len(a), len(b))
+    for i in range(n):
+        if a[i] != b[i]:
+            return f"len gpu={len(a)} oracle={len(b)}; first diff at byte {i}: {a[i]:#x} vs {b[i]:#x}"
+    return f"len gpu={len(a)} oracle={len(b)} (prefix equal)"
+
+
+def check_stream(ch, bits, rate, n, stream=0, first_frame=0, specials=True, decodable=True, **kw):
+    pcm = synth.synth_pcm(n, ch, bits, rate, stream=stream, specials=specials)
+    enc = gpu_encoder(ch, bits, rate, **kw)
+    okw = {}
+    if "stereo_decorrelation" in kw:
+        okw["stereo"] = kw["stereo_decorrelation"]
+    if "max_rice_part_order" in kw:
+        okw["part_order"] = kw["max_rice_part_order"]
+    if "max_rice_param" in kw:
+        okw["param"] = kw["max_rice_param"]
+    block = kw.get("block_size", 4096)
+    ref, ref_sizes, ref_md5 = oracle_ref.encode_stream(pcm, ch, bits, rate, block=block, first_frame=first_frame,
+                                                       **okw)
+    got, sizes = enc.encode_frames(pcm, first_frame=first_frame)
+    assert sizes == ref_sizes, "per-frame sizes differ"
+    assert got == ref, _diff_msg(got, ref)
+    if decodable:
+        dec, _ = oracle_ref.decode_frames(got, ch, bits, rate, n, first_number=first_frame)
+        assert dec == pcm
+    return pcm, got
+
+
+@pytest.mark.parametrize("ch,bits,rate", CONFIGS)
+def test_stream_parity(ch, bits, rate):
+    # 130 full blocks (includes the special blocks at 63 and 127) + a short tail
+    check_stream(ch, bits, rate, 4096 * 130 + 1000)
+
+
+@pytest.mark.parametrize("tail", [1, 2, 4, 5, 8, 16, 24, 64, 192, 255, 256, 512, 576, 1000, 1152, 2048, 4095])
+def test_tail_lengths(tail):
+    check_stream(2, 16, 44100, 4096 * 2 + tail, stream=tail)
+
+
+@pytest.mark.parametrize("ch,bits", [(1, 16), (2, 24), (2, 32), (8, 24)])
+@pytest.mark.parametrize("tail", [3, 17, 100, 333, 4000])
+def test_tail_lengths_other(ch, bits, tail):
+    check_stream(ch, bits, 48000, 4096 + tail, stream=tail)
+
+
+@pytest.mark.parametrize("first", [0, 127, 128, 2047, 2048, 65535, 65536, (1 << 21) - 1, 1 << 21, (1 << 31),
+                                   (1 << 36) - 4])
+def test_frame_numbers(first):
+    # UTF-8 coded frame numbers of every width (frame_writer.zig:235-251)
+    check_stream(2, 16, 44100, 4096 * 3 + 10, first_frame=first)
+
+
+@pytest.mark.parametrize("rate", [44100, 48000, 96000, 192000, 88200, 176400, 8000, 16000, 22050, 24000, 32000,
+                                  11025, 37800, 200, 352800])
+def test_sample_rates(rate):
+    # includes the uncommon-rate header quirk (frame_writer.zig:258-262): for rates <= 255 the
+    # reference ORs the (unmasked) block size into an 8-bit field, so its frames are not
+    # decodable FLAC; parity is byte equality with the reference behaviour there.
+    check_stream(2, 16, rate, 4096 + 300, decodable=rate > 255)
+
+
+def test_stereo_off():
+    check_stream(2, 16, 44100, 4096 * 65 + 7, stereo_decorrelation=False)
+
+
+@pytest.mark.parametrize("po,pm", [(0, 30), (4, 30), (8, 14), (8, 5), (2, 1)])
+def test_rice_caps(po, pm):
+    check_stream(2, 24, 96000, 4096 * 3 + 77, max_rice_part_order=po, max_rice_param=pm)
+
+
+def test_block_size_1152():
+    check_stream(2, 16, 44100, 1152 * 40 + 5, block_size=1152)
+
+
+def _records_match(ch, bits, rate, n, stream=0):
+    pcm = synth.synth_pcm(n, ch, bits, rate, stream=stream)
+    enc = gpu_encoder(ch, bits, rate)
+    enc.set_records(True)
+    try:
+        got, sizes = enc.encode_frames(pcm)
+        recs = enc.records()
+    finally:
+        enc.set_records(False)
+    B = bits // 8
+    samples = synth.from_pcm_bytes(pcm, ch, bits)
+    bs = 4096
+    for f, rec in enumerate(recs):
+        planes = [np.ascontiguousarray(samples[f * bs:(f + 1) * bs, c]).astype(np.int32) for c in range(ch)]
+        nn = len(planes[0])
+        ref_bytes, orec = oracle_ref.encode_frame(planes, nn, f, ch, bits, rate)
+        assert rec.channel_code == orec.channel_code, f"frame {f} channel code"
+        for c in range(orec.n_cand):
+            g, o = rec.cand[c], orec.cand[c]
+            ctx = f"frame {f} cand {c}"
+            assert (g.type, g.waste, g.bits) == (o.type, o.waste, o.bits), ctx
+            assert g.estimate == o.estimate, ctx + f" estimate {g.estimate} vs {o.estimate}"
+            if o.type == 2:
+                assert (g.order, g.part_order, g.method) == (o.order, o.part_order, o.method), ctx
+                np_ = 1 << o.part_order
+                assert list(g.params)[:np_] == list(o.params)[:np_], ctx
+            if o.type == 0:
+                assert g.constant == o.constant, ctx
+    return got
+
+
+@pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (2, 24, 96000), (2, 32, 192000), (3, 16, 48000)])
+def test_decision_records(ch, bits, rate):
+    _records_match(ch, bits, rate, 4096 * 66 + 513)
+
+
+def test_md5_matches_hashlib():
+    enc = gpu_encoder(2, 16, 44100)
+    for n in [0, 1, 55, 56, 63, 64, 65, 119, 120, 128, 1000, 65536 + 17]:
+        data = np.random.default_rng(n).integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        assert enc.md5(data) == hashlib.md5(data).digest(), n
+    # streaming updates in odd pieces
+    data = synth.synth_pcm(50000, 2, 16, 44100)
+    enc.lib.flacgpu_md5_init(enc.ctx)
+    pos = 0
+    for step in [1, 63, 64, 65, 1000, 4096 * 4]:
+        enc.md5_update(data[pos:pos + step])
+        pos += step
+    enc.md5_update(data[pos:])
+    assert enc.md5_final() == hashlib.md5(data).digest()
+
+
+def test_write_frame_planar():
+    ch, bits, rate = 2, 16, 44100
+    enc = gpu_encoder(ch, bits, rate)
+    s = synth.synth_samples(4096 * 3, ch, bits, rate, stream=9)
+    for f, n in [(0, 4096), (1, 4096), (7, 1000), (300, 5), (2, 1)]:
+        planes = [np.ascontiguousarray(s[f % 2 * 4096:f % 2 * 4096 + n, c]).astype(np.int32) for c in range(ch)]
+        got = enc.write_frame(np.stack(planes), f)
+        ref, _ = oracle_ref.encode_frame(planes, n, f, ch, bits, rate)
+        assert got == ref, (f, n, _diff_msg(got, ref))

@@ -1,0 +1,687 @@
+// fg_api.cpp -- the C ABI of libflacgpu.so (include/flacgpu.h): device
+// memory planning, frame tables, launches and host <-> device movement for
+// the gfx950 kernels in fg_kernels.hip.  No CPU encoding path exists: every
+// encode goes through the HIP kernels, and a missing/unsupported device is an
+// error (FLACGPU_ERR_DEVICE), never a fallback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/flacgpu.h"
+#include "fg_common.hpp"
+#include "fg_layout.hpp"
+
+namespace fg {
+hipError_t launch_encode(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, uint32_t stride, uint64_t first,
+                            uint32_t n_frames, hipStream_t st);
+hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, hipStream_t st);
+hipError_t launch_compact(const uint8_t *slots, uint32_t slot_bytes, const uint32_t *sizes, const uint64_t *offsets,
+                          uint8_t *out, uint64_t out_cap, uint32_t *err, uint32_t n, hipStream_t st);
+hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, uint32_t n,
+                              uint8_t *digests, hipStream_t st);
+hipError_t launch_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks, hipStream_t st);
+}  // namespace fg
+
+using namespace fg;
+
+static_assert(sizeof(SubRec) == sizeof(flacgpu_subframe_record), "record layout");
+static_assert(sizeof(FrameRec) == sizeof(flacgpu_frame_record), "record layout");
+
+namespace {
+
+constexpr uint32_t kCrcPoly = 0x8005u;
+
+uint32_t crc_mulmod_host(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int i = 15; i >= 0; i--) {
+        r <<= 1;
+        if (r & 0x10000u) r ^= 0x10000u | kCrcPoly;
+        if ((a >> i) & 1u) r ^= b;
+    }
+    return r & 0xFFFFu;
+}
+// z^e mod P
+uint32_t crc_zpow(uint64_t e) {
+    uint32_t result = 1, base = 2;  // z
+    while (e) {
+        if (e & 1) result = crc_mulmod_host(result, base);
+        base = crc_mulmod_host(base, base);
+        e >>= 1;
+    }
+    return result;
+}
+
+struct TimedLaunch {
+    int kernel;
+    hipEvent_t start, stop;
+};
+
+}  // namespace
+
+struct flacgpu_ctx {
+    int device = 0;
+    flacgpu_config cfg{};
+    uint32_t max_frames = 0;
+    uint32_t C = 0, B = 0, bits = 0, stereo = 0, nt = 0;
+    uint32_t image_bytes = 0, slot_bytes = 0, lds = 0, lds_tail = 0, crc_seg = 0;
+    hipStream_t stream = nullptr, aux = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr;
+    uint32_t *d_err = nullptr;
+    FrameJob *d_jobs = nullptr;
+    uint8_t *d_slots = nullptr;
+    uint32_t *d_fbytes = nullptr;
+    uint64_t *d_offsets = nullptr, *d_total = nullptr;
+    uint8_t *d_pcm = nullptr;
+    uint64_t pcm_cap = 0;
+    uint8_t *d_out = nullptr;
+    uint64_t out_cap = 0;
+    FrameRec *d_records = nullptr;
+    bool records_on = false;
+    std::vector<FrameRec> h_records;
+    bool timing = false;
+    std::vector<TimedLaunch> pending;
+    std::vector<hipEvent_t> event_pool;
+    uint64_t launches[FLACGPU_K_COUNT] = {};
+    double ms[FLACGPU_K_COUNT] = {};
+    // streaming MD5 (one stream)
+    uint32_t *d_md5_state = nullptr;
+    uint32_t *d_md5_blocks = nullptr;
+    uint64_t md5_block_cap = 0;
+    uint8_t md5_buf[64] = {};
+    uint32_t md5_fill = 0;
+    uint64_t md5_len = 0;
+};
+
+struct flacgpu_plan {
+    flacgpu_ctx *ctx = nullptr;
+    uint32_t n_streams = 0;
+    uint32_t B = 0;
+    uint64_t n_frames = 0, n_full = 0, n_tail = 0;
+    FrameJob *d_jobs = nullptr;  // full jobs first, then tail jobs
+    uint64_t *d_md5_offs = nullptr, *d_md5_lens = nullptr;
+    std::vector<uint64_t> first_frame;
+    uint64_t out_bound = 0;
+    uint8_t *d_slots = nullptr;  // per-plan slot area when larger than the context's
+    uint32_t *d_fbytes = nullptr;
+    uint64_t slots_frames = 0;
+};
+
+namespace {
+
+hipEvent_t get_event(flacgpu_ctx *c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+void resolve_timing(flacgpu_ctx *c) {
+    for (auto &t : c->pending) {
+        hipEventSynchronize(t.stop);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, t.start, t.stop) == hipSuccess) {
+            c->launches[t.kernel]++;
+            c->ms[t.kernel] += ms;
+        }
+        c->event_pool.push_back(t.start);
+        c->event_pool.push_back(t.stop);
+    }
+    c->pending.clear();
+}
+
+struct Timed {
+    flacgpu_ctx *c;
+    int k;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    Timed(flacgpu_ctx *c_, int k_, hipStream_t st_) : c(c_), k(k_), st(st_) {
+        if (c->timing) {
+            a = get_event(c);
+            b = get_event(c);
+            if (a) hipEventRecord(a, st);
+        }
+    }
+    ~Timed() {
+        if (c->timing && a && b) {
+            hipEventRecord(b, st);
+            c->pending.push_back({k, a, b});
+        }
+    }
+};
+
+int hip_err(hipError_t e) { return e == hipSuccess ? FLACGPU_OK : (e == hipErrorOutOfMemory ? FLACGPU_ERR_OUT_OF_MEMORY : FLACGPU_ERR_DEVICE); }
+
+#define HIPCHK(x)                               \
+    do {                                        \
+        hipError_t e_ = (x);                    \
+        if (e_ != hipSuccess) return hip_err(e_); \
+    } while (0)
+
+int validate(const flacgpu_config *cfg) {
+    if (!cfg) return FLACGPU_ERR_INVALID_INPUT;
+    if (cfg->channels < 1 || cfg->channels > 8) return FLACGPU_ERR_INVALID_CONFIG;
+    const uint32_t b = cfg->bits_per_sample;
+    if (b != 8 && b != 16 && b != 24 && b != 32) return FLACGPU_ERR_INVALID_CONFIG;  // frame_writer.zig:221-233
+    if (cfg->block_size < 1 || cfg->block_size > kBlock) return FLACGPU_ERR_INVALID_CONFIG;
+    if (cfg->max_rice_part_order > kMaxPartOrder) return FLACGPU_ERR_INVALID_CONFIG;  // rice.zig:13 buffers
+    if (cfg->max_rice_param < 1 || cfg->max_rice_param > 30) return FLACGPU_ERR_INVALID_CONFIG;
+    if (cfg->sample_rate >= (1u << 20)) return FLACGPU_ERR_INVALID_CONFIG;  // u20 (wav_reader.zig:98)
+    if (cfg->prediction != 0) return FLACGPU_ERR_INVALID_CONFIG;  // only fixed prediction exists
+    return FLACGPU_OK;
+}
+
+uint64_t frames_for(uint64_t n_samples, uint32_t bs) { return (n_samples + bs - 1) / bs; }
+
+// Queue the encode of n_full full frames (jobs[0..n_full)) and n_tail short ones
+// (jobs[n_full..)), then scan + compact into d_out.
+int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, uint64_t n_full, uint64_t n_tail,
+                uint8_t *d_slots, uint32_t *d_fbytes, uint8_t *d_out, uint64_t out_cap, uint64_t *d_offsets,
+                uint64_t *d_total, hipStream_t st) {
+    const uint64_t n_frames = n_full + n_tail;
+    if (n_frames == 0) {
+        HIPCHK(hipMemsetAsync(d_total, 0, sizeof(uint64_t), st));
+        return FLACGPU_OK;
+    }
+    if (n_frames > 0xFFFFFFFFull) return FLACGPU_ERR_INVALID_INPUT;
+    EncodeArgs a{};
+    a.pcm = d_pcm;
+    a.channels = c->C;
+    a.bits = c->bits;
+    a.bytes_per_sample = c->B;
+    a.sample_rate = c->cfg.sample_rate;
+    a.stereo = c->stereo;
+    a.max_part_order = c->cfg.max_rice_part_order;
+    a.max_param = c->cfg.max_rice_param;
+    a.block_size = c->cfg.block_size;
+    a.slots = d_slots;
+    a.slot_bytes = c->slot_bytes;
+    a.image_bytes = c->image_bytes;
+    a.frame_bytes = d_fbytes;
+    a.err = c->d_err;
+    a.crc_tab = c->d_crc_tab;
+    a.crc_pow = c->d_crc_pow;
+    a.crc_seg_words = c->crc_seg;
+    a.records = c->records_on ? c->d_records : nullptr;
+    if (n_full) {
+        Timed t(c, FLACGPU_K_ENCODE, st);
+        a.jobs = d_jobs;
+        a.n_jobs = (uint32_t)n_full;
+        HIPCHK(launch_encode(a, true, c->nt, c->lds, st));
+    }
+    if (n_tail) {
+        Timed t(c, FLACGPU_K_ENCODE_TAIL, st);
+        a.jobs = d_jobs + n_full;
+        a.n_jobs = (uint32_t)n_tail;
+        HIPCHK(launch_encode(a, false, c->nt, c->lds_tail, st));
+    }
+    {
+        Timed t(c, FLACGPU_K_SCAN, st);
+        HIPCHK(launch_scan(d_fbytes, d_offsets, d_total, (uint32_t)n_frames, st));
+    }
+    {
+        Timed t(c, FLACGPU_K_COMPACT, st);
+        HIPCHK(launch_compact(d_slots, c->slot_bytes, d_fbytes, d_offsets, d_out, out_cap, c->d_err,
+                              (uint32_t)n_frames, st));
+    }
+    return FLACGPU_OK;
+}
+
+int check_device_error(flacgpu_ctx *c) {
+    uint32_t err = 0;
+    HIPCHK(hipMemcpy(&err, c->d_err, 4, hipMemcpyDeviceToHost));
+    if (err) {
+        hipMemset(c->d_err, 0, 4);
+        return (err & 2u) ? FLACGPU_ERR_OUTPUT_TOO_SMALL : FLACGPU_ERR_INTERNAL;
+    }
+    return FLACGPU_OK;
+}
+
+int fetch_records(flacgpu_ctx *c, uint64_t n_frames, hipStream_t st) {
+    if (!c->records_on) return FLACGPU_OK;
+    const size_t base = c->h_records.size();
+    c->h_records.resize(base + n_frames);
+    HIPCHK(hipMemcpyAsync(c->h_records.data() + base, c->d_records, n_frames * sizeof(FrameRec),
+                          hipMemcpyDeviceToHost, st));
+    return FLACGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+flacgpu_config flacgpu_config_default(uint32_t channels, uint32_t bits_per_sample, uint32_t sample_rate) {
+    flacgpu_config c{};
+    c.sample_rate = sample_rate;
+    c.block_size = 4096;
+    c.channels = (uint8_t)channels;
+    c.bits_per_sample = (uint8_t)bits_per_sample;
+    c.stereo_decorrelation = 1;
+    c.max_rice_part_order = 8;
+    c.max_rice_param = 30;
+    c.prediction = 0;
+    return c;
+}
+
+const char *flacgpu_strerror(int code) {
+    switch (code) {
+        case FLACGPU_OK: return "ok";
+        case FLACGPU_ERR_INVALID_CONFIG: return "invalid config";
+        case FLACGPU_ERR_INVALID_INPUT: return "invalid input";
+        case FLACGPU_ERR_OUT_OF_MEMORY: return "out of memory";
+        case FLACGPU_ERR_OUTPUT_TOO_SMALL: return "output buffer too small";
+        case FLACGPU_ERR_DEVICE: return "HIP device error (no usable gfx950 device?)";
+        case FLACGPU_ERR_INTERNAL: return "device-side invariant violated";
+        default: return "unknown error";
+    }
+}
+
+int flacgpu_abi_version(void) { return FLACGPU_ABI_VERSION; }
+
+size_t flacgpu_reference_max_frame_bytes(const flacgpu_config *cfg) {
+    if (!cfg) return 0;
+    // maxFrameBytes(block_size, bit_depth, channels, compute_waste_bits=true) (encoder.zig:55-60,583-595)
+    const size_t bps = cfg->channels == 2 ? cfg->bits_per_sample + 1u : cfg->bits_per_sample;
+    return 14u + 8u * cfg->channels + (size_t)cfg->block_size * ((bps + 7) / 8) * (cfg->channels + 1u) + 2u;
+}
+
+size_t flacgpu_frame_bound_bytes(const flacgpu_config *cfg) {
+    if (!cfg) return 0;
+    const bool stereo = cfg->channels == 2 && cfg->stereo_decorrelation;
+    return frame_bound_bytes(kBlock, cfg->channels, cfg->bits_per_sample, stereo);
+}
+
+int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_call, flacgpu_ctx **out) {
+    if (!out) return FLACGPU_ERR_INVALID_INPUT;
+    *out = nullptr;
+    int rc = validate(cfg);
+    if (rc) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return FLACGPU_ERR_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FLACGPU_ERR_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FLACGPU_ERR_DEVICE;  // code objects are gfx950-only
+    HIPCHK(hipSetDevice(device));
+
+    auto *c = new (std::nothrow) flacgpu_ctx();
+    if (!c) return FLACGPU_ERR_OUT_OF_MEMORY;
+    c->device = device;
+    c->cfg = *cfg;
+    c->max_frames = max_frames_per_call ? max_frames_per_call : 32768u;
+    c->C = cfg->channels;
+    c->bits = cfg->bits_per_sample;
+    c->B = c->bits / 8;
+    c->stereo = (c->C == 2 && cfg->stereo_decorrelation) ? 1u : 0u;
+    const uint32_t nw = c->stereo ? 4u : c->C;
+    c->nt = 64u * nw;
+    c->image_bytes = fg_round16(frame_bound_bytes(kBlock, c->C, c->bits, c->stereo != 0));
+    c->slot_bytes = (c->image_bytes + 16u + 255u) & ~255u;
+    c->lds = lds_layout(c->C, c->B, nw, c->image_bytes, true).total;
+    c->lds_tail = lds_layout(c->C, c->B, nw, c->image_bytes, false).total;
+    c->crc_seg = (c->image_bytes / 4u + c->nt - 1u) / c->nt;
+    if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u) {
+        delete c;
+        return FLACGPU_ERR_INVALID_CONFIG;
+    }
+
+    auto fail = [&](int code) {
+        flacgpu_close(c);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+
+    // CRC-16 tables: x * z^e mod P for e = 40, 32, 24, 16 (see crc_word in the kernels)
+    std::vector<uint16_t> tab(1024);
+    const uint32_t ze[4] = {crc_zpow(40), crc_zpow(32), crc_zpow(24), crc_zpow(16)};
+    for (int t = 0; t < 4; t++)
+        for (uint32_t x = 0; x < 256; x++) tab[t * 256 + x] = (uint16_t)crc_mulmod_host(x, ze[t]);
+    std::vector<uint16_t> pw(c->nt);
+    for (uint32_t t = 0; t < c->nt; t++) pw[t] = (uint16_t)crc_zpow(32ull * c->crc_seg * (c->nt - 1u - t));
+
+    const uint64_t F = c->max_frames;
+    c->pcm_cap = F * (uint64_t)kBlock * c->C * c->B + 64;
+    c->out_cap = F * (uint64_t)c->slot_bytes;
+    if (hipMalloc(&c->d_crc_tab, 1024 * 2) || hipMalloc(&c->d_crc_pow, c->nt * 2) || hipMalloc(&c->d_err, 16) ||
+        hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_slots, F * (uint64_t)c->slot_bytes) ||
+        hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
+        hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16))
+        return fail(FLACGPU_ERR_OUT_OF_MEMORY);
+    if (hipMemcpy(c->d_crc_tab, tab.data(), 2048, hipMemcpyHostToDevice) ||
+        hipMemcpy(c->d_crc_pow, pw.data(), c->nt * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16))
+        return fail(FLACGPU_ERR_DEVICE);
+    flacgpu_md5_init(c);
+    *out = c;
+    return FLACGPU_OK;
+}
+
+void flacgpu_close(flacgpu_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    resolve_timing(c);
+    for (auto e : c->event_pool) hipEventDestroy(e);
+    hipFree(c->d_crc_tab);
+    hipFree(c->d_crc_pow);
+    hipFree(c->d_err);
+    hipFree(c->d_jobs);
+    hipFree(c->d_slots);
+    hipFree(c->d_fbytes);
+    hipFree(c->d_offsets);
+    hipFree(c->d_total);
+    hipFree(c->d_pcm);
+    hipFree(c->d_out);
+    hipFree(c->d_records);
+    hipFree(c->d_md5_state);
+    hipFree(c->d_md5_blocks);
+    if (c->fork) hipEventDestroy(c->fork);
+    if (c->join) hipEventDestroy(c->join);
+    if (c->aux) hipStreamDestroy(c->aux);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
+                          uint64_t first_frame_number, uint8_t *out, size_t out_cap, size_t *out_len,
+                          uint32_t *frame_bytes) {
+    if (!c || (!pcm && n_samples) || !out_len) return FLACGPU_ERR_INVALID_INPUT;
+    if (bytes_per_sample != c->B) return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    *out_len = 0;
+    const uint32_t bs = c->cfg.block_size;
+    const uint64_t stride = (uint64_t)bs * c->C * c->B;
+    const uint64_t total_frames = frames_for(n_samples, bs);
+    // frame numbers are u36 (frame_writer.zig:153, wav2flac.zig:75)
+    if (total_frames && (first_frame_number >= (1ull << 36) || total_frames - 1 > (1ull << 36) - 1 - first_frame_number))
+        return FLACGPU_ERR_INVALID_INPUT;
+    const uint8_t *src = (const uint8_t *)pcm;
+    uint64_t frame0 = 0;
+    size_t written = 0;
+    if (c->records_on) c->h_records.clear();
+    while (frame0 < total_frames) {
+        const uint64_t nf = std::min<uint64_t>(c->max_frames, total_frames - frame0);
+        const uint64_t s0 = frame0 * bs;
+        const uint64_t ns = std::min<uint64_t>(nf * bs, n_samples - s0);
+        const uint64_t nbytes = ns * c->C * c->B;
+        HIPCHK(hipMemcpyAsync(c->d_pcm, src + s0 * c->C * c->B, nbytes, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, first_frame_number + frame0, (uint32_t)nf,
+                                c->stream));
+        // frames with n == 4096 take the lane-owned-partition kernel, the rest the general one
+        uint64_t n_full = (bs == (uint32_t)kBlock) ? ns / kBlock : 0;
+        int rc = encode_core(c, c->d_pcm, c->d_jobs, n_full, nf - n_full, c->d_slots, c->d_fbytes, c->d_out,
+                             c->out_cap, c->d_offsets, c->d_total, c->stream);
+        if (rc) return rc;
+        uint64_t total = 0;
+        HIPCHK(hipMemcpyAsync(&total, c->d_total, 8, hipMemcpyDeviceToHost, c->stream));
+        if (frame_bytes)
+            HIPCHK(hipMemcpyAsync(frame_bytes + frame0, c->d_fbytes, nf * 4, hipMemcpyDeviceToHost, c->stream));
+        if ((rc = fetch_records(c, nf, c->stream))) return rc;
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if ((rc = check_device_error(c))) return rc;
+        if (written + total > out_cap) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
+        HIPCHK(hipMemcpy(out + written, c->d_out, total, hipMemcpyDeviceToHost));
+        written += total;
+        frame0 += nf;
+    }
+    resolve_timing(c);
+    *out_len = written;
+    return FLACGPU_OK;
+}
+
+int flacgpu_encode_frame_planar(flacgpu_ctx *c, const int32_t *const planes[8], uint32_t n, uint64_t frame_number,
+                                uint8_t *out, size_t out_cap, uint32_t *frame_bytes) {
+    if (!c || !planes || !out || n == 0 || n > c->cfg.block_size) return FLACGPU_ERR_INVALID_INPUT;
+    for (uint32_t ch = 0; ch < c->C; ch++)
+        if (!planes[ch]) return FLACGPU_ERR_INVALID_INPUT;
+    // Encoder.samples[ch][0..n] -> the little-endian interleaved layout the kernels stage
+    std::vector<uint8_t> pcm((size_t)n * c->C * c->B + 4);
+    for (uint32_t i = 0; i < n; i++)
+        for (uint32_t ch = 0; ch < c->C; ch++) {
+            const uint32_t v = (uint32_t)planes[ch][i];
+            uint8_t *d = &pcm[((size_t)i * c->C + ch) * c->B];
+            for (uint32_t k = 0; k < c->B; k++) d[k] = (uint8_t)(v >> (8 * k));
+        }
+    size_t len = 0;
+    uint32_t fb = 0;
+    int rc = flacgpu_encode_frames(c, pcm.data(), c->B, n, frame_number, out, out_cap, &len, &fb);
+    if (rc) return rc;
+    if (frame_bytes) *frame_bytes = fb;
+    return FLACGPU_OK;
+}
+
+// ---- streaming MD5 --------------------------------------------------------
+int flacgpu_md5_init(flacgpu_ctx *c) {
+    if (!c) return FLACGPU_ERR_INVALID_INPUT;
+    const uint32_t iv[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(c->d_md5_state, iv, 16, hipMemcpyHostToDevice));
+    c->md5_fill = 0;
+    c->md5_len = 0;
+    return FLACGPU_OK;
+}
+
+static int md5_push_blocks(flacgpu_ctx *c, const uint8_t *p, uint64_t nblocks) {
+    if (!nblocks) return FLACGPU_OK;
+    if (nblocks > c->md5_block_cap) {
+        hipFree(c->d_md5_blocks);
+        c->d_md5_blocks = nullptr;
+        c->md5_block_cap = 0;
+        HIPCHK(hipMalloc(&c->d_md5_blocks, nblocks * 64));
+        c->md5_block_cap = nblocks;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_md5_blocks, p, nblocks * 64, hipMemcpyHostToDevice, c->stream));
+    {
+        Timed t(c, FLACGPU_K_MD5, c->stream);
+        HIPCHK(launch_md5_blocks(c->d_md5_state, c->d_md5_blocks, nblocks, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FLACGPU_OK;
+}
+
+int flacgpu_md5_update(flacgpu_ctx *c, const void *data, size_t len) {
+    if (!c || (!data && len)) return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    const uint8_t *p = (const uint8_t *)data;
+    c->md5_len += len;
+    if (c->md5_fill) {
+        const size_t take = std::min<size_t>(64 - c->md5_fill, len);
+        std::memcpy(c->md5_buf + c->md5_fill, p, take);
+        c->md5_fill += (uint32_t)take;
+        p += take;
+        len -= take;
+        if (c->md5_fill == 64) {
+            int rc = md5_push_blocks(c, c->md5_buf, 1);
+            if (rc) return rc;
+            c->md5_fill = 0;
+        }
+    }
+    const uint64_t nb = len / 64;
+    int rc = md5_push_blocks(c, p, nb);
+    if (rc) return rc;
+    p += nb * 64;
+    len -= nb * 64;
+    std::memcpy(c->md5_buf, p, len);
+    c->md5_fill = (uint32_t)len;
+    return FLACGPU_OK;
+}
+
+int flacgpu_md5_final(flacgpu_ctx *c, uint8_t digest[16]) {
+    if (!c || !digest) return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    uint8_t tail[128] = {};
+    std::memcpy(tail, c->md5_buf, c->md5_fill);
+    tail[c->md5_fill] = 0x80;
+    const uint32_t nb = c->md5_fill < 56 ? 1 : 2;
+    const uint64_t bits = c->md5_len * 8;
+    for (int i = 0; i < 8; i++) tail[nb * 64 - 8 + i] = (uint8_t)(bits >> (8 * i));
+    int rc = md5_push_blocks(c, tail, nb);
+    if (rc) return rc;
+    uint32_t st[4];
+    HIPCHK(hipMemcpy(st, c->d_md5_state, 16, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) digest[4 * i + j] = (uint8_t)(st[i] >> (8 * j));
+    resolve_timing(c);
+    return flacgpu_md5_init(c);
+}
+
+// ---- plans (device-resident batches of independent streams) --------------
+int flacgpu_plan_create(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs, const uint64_t *samples,
+                        uint32_t bytes_per_sample, flacgpu_plan **out) {
+    if (!c || !out || (n_streams && (!offs || !samples)) || bytes_per_sample != c->B) return FLACGPU_ERR_INVALID_INPUT;
+    *out = nullptr;
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t bs = c->cfg.block_size;
+    const uint64_t fbytes_in = (uint64_t)c->C * c->B;
+    std::vector<FrameJob> full, tail;
+    std::vector<uint64_t> lens(n_streams);
+    auto *p = new (std::nothrow) flacgpu_plan();
+    if (!p) return FLACGPU_ERR_OUT_OF_MEMORY;
+    p->ctx = c;
+    p->n_streams = n_streams;
+    p->B = bytes_per_sample;
+    p->first_frame.resize(n_streams);
+    uint64_t slot = 0;
+    for (uint32_t s = 0; s < n_streams; s++) {
+        if (offs[s] & 3u) {
+            delete p;
+            return FLACGPU_ERR_INVALID_INPUT;
+        }
+        p->first_frame[s] = slot;
+        lens[s] = samples[s] * fbytes_in;
+        const uint64_t nf = frames_for(samples[s], bs);
+        for (uint64_t f = 0; f < nf; f++, slot++) {
+            FrameJob j;
+            j.pcm_off = offs[s] + f * bs * fbytes_in;
+            j.number = f;
+            j.n = (uint32_t)std::min<uint64_t>(bs, samples[s] - f * bs);
+            j.slot = (uint32_t)slot;
+            (j.n == (uint32_t)kBlock ? full : tail).push_back(j);
+        }
+    }
+    p->n_frames = slot;
+    p->n_full = full.size();
+    p->n_tail = tail.size();
+    p->out_bound = slot * (uint64_t)c->slot_bytes;
+    full.insert(full.end(), tail.begin(), tail.end());
+    auto fail = [&](int code) {
+        flacgpu_plan_destroy(p);
+        return code;
+    };
+    if (slot) {
+        if (hipMalloc(&p->d_jobs, slot * sizeof(FrameJob))) return fail(FLACGPU_ERR_OUT_OF_MEMORY);
+        if (hipMemcpy(p->d_jobs, full.data(), slot * sizeof(FrameJob), hipMemcpyHostToDevice))
+            return fail(FLACGPU_ERR_DEVICE);
+    }
+    if (n_streams) {
+        if (hipMalloc(&p->d_md5_offs, n_streams * 8) || hipMalloc(&p->d_md5_lens, n_streams * 8))
+            return fail(FLACGPU_ERR_OUT_OF_MEMORY);
+        if (hipMemcpy(p->d_md5_offs, offs, n_streams * 8, hipMemcpyHostToDevice) ||
+            hipMemcpy(p->d_md5_lens, lens.data(), n_streams * 8, hipMemcpyHostToDevice))
+            return fail(FLACGPU_ERR_DEVICE);
+    }
+    if (slot > c->max_frames) {
+        if (hipMalloc(&p->d_slots, slot * (uint64_t)c->slot_bytes) || hipMalloc(&p->d_fbytes, slot * 4))
+            return fail(FLACGPU_ERR_OUT_OF_MEMORY);
+        p->slots_frames = slot;
+    }
+    *out = p;
+    return FLACGPU_OK;
+}
+
+void flacgpu_plan_destroy(flacgpu_plan *p) {
+    if (!p) return;
+    hipFree(p->d_jobs);
+    hipFree(p->d_md5_offs);
+    hipFree(p->d_md5_lens);
+    hipFree(p->d_slots);
+    hipFree(p->d_fbytes);
+    delete p;
+}
+
+uint64_t flacgpu_plan_frames(const flacgpu_plan *p) { return p ? p->n_frames : 0; }
+uint64_t flacgpu_plan_out_bound(const flacgpu_plan *p) { return p ? p->out_bound : 0; }
+uint64_t flacgpu_plan_stream_first_frame(const flacgpu_plan *p, uint32_t s) {
+    return (p && s < p->n_streams) ? p->first_frame[s] : 0;
+}
+
+int flacgpu_encode_plan_device(flacgpu_ctx *c, const flacgpu_plan *p, const void *d_pcm, uint8_t *d_out,
+                               uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets, uint64_t *d_total,
+                               uint8_t *d_md5, void *hip_stream) {
+    if (!c || !p || p->ctx != c || !d_pcm || !d_out || !d_frame_bytes || !d_frame_offsets || !d_total)
+        return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    if (c->records_on && p->n_frames > c->max_frames) return FLACGPU_ERR_INVALID_INPUT;
+    uint8_t *slots = p->d_slots ? p->d_slots : c->d_slots;
+    // MD5 of every stream on the auxiliary stream, overlapping the encode kernels
+    if (d_md5 && p->n_streams) {
+        HIPCHK(hipEventRecord(c->fork, st));
+        HIPCHK(hipStreamWaitEvent(c->aux, c->fork, 0));
+        {
+            Timed t(c, FLACGPU_K_MD5, c->aux);
+            HIPCHK(launch_md5_streams((const uint8_t *)d_pcm, p->d_md5_offs, p->d_md5_lens, p->n_streams, d_md5,
+                                      c->aux));
+        }
+        HIPCHK(hipEventRecord(c->join, c->aux));
+    }
+    int rc = encode_core(c, (const uint8_t *)d_pcm, p->d_jobs, p->n_full, p->n_tail, slots, d_frame_bytes, d_out,
+                         out_cap, d_frame_offsets, d_total, st);
+    if (rc) return rc;
+    if (d_md5 && p->n_streams) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
+    return FLACGPU_OK;
+}
+
+// ---- instrumentation ---------------------------------------------------------
+int flacgpu_set_timing(flacgpu_ctx *c, int enable) {
+    if (!c) return FLACGPU_ERR_INVALID_INPUT;
+    c->timing = enable != 0;
+    return FLACGPU_OK;
+}
+
+int flacgpu_kernel_time(flacgpu_ctx *c, int kernel, uint64_t *launches, double *total_ms) {
+    if (!c || kernel < 0 || kernel >= FLACGPU_K_COUNT) return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    resolve_timing(c);
+    if (launches) *launches = c->launches[kernel];
+    if (total_ms) *total_ms = c->ms[kernel];
+    return FLACGPU_OK;
+}
+
+int flacgpu_reset_timing(flacgpu_ctx *c) {
+    if (!c) return FLACGPU_ERR_INVALID_INPUT;
+    resolve_timing(c);
+    for (int k = 0; k < FLACGPU_K_COUNT; k++) {
+        c->launches[k] = 0;
+        c->ms[k] = 0;
+    }
+    return FLACGPU_OK;
+}
+
+int flacgpu_set_records(flacgpu_ctx *c, int enable) {
+    if (!c) return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    if (enable && !c->d_records) HIPCHK(hipMalloc(&c->d_records, (uint64_t)c->max_frames * sizeof(FrameRec)));
+    if (enable) HIPCHK(hipMemset(c->d_records, 0, (uint64_t)c->max_frames * sizeof(FrameRec)));
+    c->records_on = enable != 0;
+    return FLACGPU_OK;
+}
+
+int flacgpu_get_records(flacgpu_ctx *c, flacgpu_frame_record *out, uint64_t max_frames, uint64_t *n_frames) {
+    if (!c || !n_frames) return FLACGPU_ERR_INVALID_INPUT;
+    const uint64_t n = std::min<uint64_t>(max_frames, c->h_records.size());
+    if (out && n) std::memcpy(out, c->h_records.data(), n * sizeof(FrameRec));
+    *n_frames = c->h_records.size();
+    return FLACGPU_OK;
+}
+
+}  // extern "C"

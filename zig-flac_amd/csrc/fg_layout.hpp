@@ -1,0 +1,56 @@
+// fg_layout.hpp -- LDS layout and size bounds shared by host and device.
+#pragma once
+#include <stdint.h>
+
+namespace fg {
+
+struct LdsLayout {
+    uint32_t img;    // frame image (BE 32-bit words), aliased with the PCM staging area
+    uint32_t par;    // rice params, kParamBytes per candidate wave
+    uint32_t rec;    // 16 x u32 per candidate wave
+    uint32_t crc;    // 4 x 256 u16 CRC tables
+    uint32_t misc;   // 64 x u32 scratch (sub lengths, crc partials, header bits)
+    uint32_t psum;   // tail kernel only: 2 x 256 u64 per wave (inside region 0)
+    uint32_t pmax;   // tail kernel only: 2 x 256 u32 per wave (inside region 0)
+    uint32_t total;
+};
+
+__host__ __device__ inline uint32_t fg_round16(uint32_t x) { return (x + 15u) & ~15u; }
+
+// Staging: 64 chunks of (16*C*B + 1) dwords (one pad dword per 64-sample chunk
+// makes the per-lane sample reads bank-conflict free).
+__host__ __device__ inline uint32_t stage_bytes(uint32_t C, uint32_t B) { return 64u * (16u * C * B + 1u) * 4u; }
+
+// Region 0 holds, in turn: the PCM staging area, (tail kernel) the per-wave
+// partition-sum tables during analysis, then the zeroed frame image.
+__host__ __device__ inline LdsLayout lds_layout(uint32_t C, uint32_t B, uint32_t nw, uint32_t image_bytes, bool full) {
+    LdsLayout L;
+    uint32_t r0 = stage_bytes(C, B);
+    if (image_bytes > r0) r0 = image_bytes;
+    if (!full && nw * 6144u > r0) r0 = nw * 6144u;
+    r0 = fg_round16(r0);
+    L.img = 0;
+    L.psum = 0;                       // tail kernel: 2 x 256 u64 per wave
+    L.pmax = nw * 4096u;              // tail kernel: 2 x 256 u32 per wave
+    L.par = r0;
+    L.rec = L.par + nw * 512u;
+    L.crc = L.rec + nw * 64u;
+    L.misc = L.crc + 2048u;
+    L.total = fg_round16(L.misc + 256u);
+    return L;
+}
+
+// Upper bound (bytes) of one encoded frame, block n <= 4096:
+// header <= 16 B; per subframe <= 14 + 4*bd + n*bd + n/2 bits (a FIXED subframe
+// is chosen only when its estimate < n*bps', and the exact Rice length exceeds
+// the estimate by at most floor(len/2) per partition); pad + CRC-16.
+__host__ __device__ inline uint32_t frame_bound_bytes(uint32_t n, uint32_t C, uint32_t bits, bool stereo) {
+    uint64_t b = 16u * 8u;
+    for (uint32_t c = 0; c < C; c++) {
+        uint32_t bd = bits + ((stereo && c == 1) ? 1u : 0u);
+        b += 14u + 4u * bd + (uint64_t)n * bd + n / 2u;
+    }
+    return (uint32_t)((b + 7u) / 8u + 1u + 2u + 16u);
+}
+
+}  // namespace fg

@@ -1,0 +1,297 @@
+"""ctypes binding of libflacgpu.so (include/flacgpu.h) for tests and the benchmark.
+
+This is plumbing over the C ABI: every encode runs in the gfx950 HIP kernels
+of libflacgpu.so.  There is no CPU fallback -- if the library or a gfx950
+device is missing, construction raises.
+
+The class names mirror the reference's Zig interface (src/lib.zig):
+`Encoder.write_frame` is `Encoder.writeFrame` (src/lib/encoder.zig:234),
+`Config.default` is `Config.default` (encoder.zig:642-655).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libflacgpu.so")
+
+OK = 0
+ERRORS = {
+    -1: "InvalidConfig",
+    -2: "InvalidInput",
+    -3: "OutOfMemory",
+    -4: "WriteFailed (output too small)",
+    -5: "DeviceError",
+    -6: "InternalError",
+}
+
+K_ENCODE, K_ENCODE_TAIL, K_SCAN, K_COMPACT, K_MD5 = range(5)
+KERNEL_NAMES = ["encode", "encode_tail", "scan", "compact", "md5"]
+
+
+class FlacGpuError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        super().__init__(f"{where}: {ERRORS.get(code, code)} ({code})")
+        self.code = code
+
+
+class Config(ctypes.Structure):
+    """flacgpu_config == Encoder.Config + Feature (encoder.zig:609-656)."""
+
+    _fields_ = [
+        ("sample_rate", ctypes.c_uint32),
+        ("block_size", ctypes.c_uint16),
+        ("channels", ctypes.c_uint8),
+        ("bits_per_sample", ctypes.c_uint8),
+        ("stereo_decorrelation", ctypes.c_uint8),
+        ("max_rice_part_order", ctypes.c_uint8),
+        ("max_rice_param", ctypes.c_uint8),
+        ("prediction", ctypes.c_uint8),
+    ]
+
+    @classmethod
+    def default(cls, channels: int, bits: int, sample_rate: int) -> "Config":
+        return cls(sample_rate, 4096, channels, bits, 1, 8, 30, 0)
+
+
+class SubframeRecord(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_uint8),
+        ("waste", ctypes.c_uint8),
+        ("bits", ctypes.c_uint8),
+        ("order", ctypes.c_uint8),
+        ("part_order", ctypes.c_uint8),
+        ("method", ctypes.c_uint8),
+        ("written", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8),
+        ("pad2", ctypes.c_uint32),
+        ("estimate", ctypes.c_uint64),
+        ("constant", ctypes.c_int64),
+        ("params", ctypes.c_uint8 * 256),
+    ]
+
+
+class FrameRecord(ctypes.Structure):
+    _fields_ = [
+        ("channel_code", ctypes.c_uint32),
+        ("n_cand", ctypes.c_uint32),
+        ("frame_bytes", ctypes.c_uint32),
+        ("pad", ctypes.c_uint32),
+        ("cand", SubframeRecord * 8),
+    ]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libflacgpu.so; raise (never fall back) if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built: run `make -C zig-flac_amd` (or __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    P, U32, U64, I32, SZ = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
+    sig = {
+        "flacgpu_config_default": (Config, [U32, U32, U32]),
+        "flacgpu_open": (I32, [I32, ctypes.POINTER(Config), U32, ctypes.POINTER(P)]),
+        "flacgpu_close": (None, [P]),
+        "flacgpu_strerror": (ctypes.c_char_p, [I32]),
+        "flacgpu_abi_version": (I32, []),
+        "flacgpu_reference_max_frame_bytes": (SZ, [ctypes.POINTER(Config)]),
+        "flacgpu_frame_bound_bytes": (SZ, [ctypes.POINTER(Config)]),
+        "flacgpu_encode_frames": (I32, [P, P, U32, U64, U64, P, SZ, ctypes.POINTER(SZ), P]),
+        "flacgpu_encode_frame_planar": (I32, [P, P, U32, U64, P, SZ, ctypes.POINTER(U32)]),
+        "flacgpu_md5_init": (I32, [P]),
+        "flacgpu_md5_update": (I32, [P, P, SZ]),
+        "flacgpu_md5_final": (I32, [P, P]),
+        "flacgpu_plan_create": (I32, [P, U32, P, P, U32, ctypes.POINTER(P)]),
+        "flacgpu_plan_destroy": (None, [P]),
+        "flacgpu_plan_frames": (U64, [P]),
+        "flacgpu_plan_out_bound": (U64, [P]),
+        "flacgpu_plan_stream_first_frame": (U64, [P, U32]),
+        "flacgpu_encode_plan_device": (I32, [P, P, P, P, U64, P, P, P, P, P]),
+        "flacgpu_set_timing": (I32, [P, I32]),
+        "flacgpu_kernel_time": (I32, [P, I32, ctypes.POINTER(U64), ctypes.POINTER(ctypes.c_double)]),
+        "flacgpu_reset_timing": (I32, [P]),
+        "flacgpu_set_records": (I32, [P, I32]),
+        "flacgpu_get_records": (I32, [P, P, U64, ctypes.POINTER(U64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def exported_symbols() -> list:
+    return [
+        "flacgpu_config_default", "flacgpu_open", "flacgpu_close", "flacgpu_strerror", "flacgpu_abi_version",
+        "flacgpu_reference_max_frame_bytes", "flacgpu_frame_bound_bytes", "flacgpu_encode_frames",
+        "flacgpu_encode_frame_planar", "flacgpu_md5_init", "flacgpu_md5_update", "flacgpu_md5_final",
+        "flacgpu_plan_create", "flacgpu_plan_destroy", "flacgpu_plan_frames", "flacgpu_plan_out_bound",
+        "flacgpu_plan_stream_first_frame", "flacgpu_encode_plan_device", "flacgpu_set_timing",
+        "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_get_records",
+    ]
+
+
+def _check(rc: int, where: str) -> None:
+    if rc != OK:
+        raise FlacGpuError(rc, where)
+
+
+class Plan:
+    def __init__(self, enc: "Encoder", offsets: Sequence[int], samples: Sequence[int]):
+        self.enc = enc
+        n = len(offsets)
+        self._offs = (ctypes.c_uint64 * max(n, 1))(*offsets)
+        self._samp = (ctypes.c_uint64 * max(n, 1))(*samples)
+        h = ctypes.c_void_p()
+        _check(enc.lib.flacgpu_plan_create(enc.ctx, n, self._offs, self._samp, enc.bytes_per_sample,
+                                           ctypes.byref(h)), "plan_create")
+        self.handle = h
+        self.n_streams = n
+        self.n_frames = enc.lib.flacgpu_plan_frames(h)
+        self.out_bound = enc.lib.flacgpu_plan_out_bound(h)
+        self.first_frame = [enc.lib.flacgpu_plan_stream_first_frame(h, s) for s in range(n)]
+
+    def close(self) -> None:
+        if self.handle:
+            self.enc.lib.flacgpu_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Encoder:
+    """GPU block encoder context == Encoder.init / deinit (encoder.zig:44-164)."""
+
+    def __init__(self, channels: int, bits: int, sample_rate: int, device: int = 0, max_frames: int = 32768,
+                 block_size: int = 4096, stereo_decorrelation: bool = True, max_rice_part_order: int = 8,
+                 max_rice_param: int = 30):
+        self.lib = load_library()
+        self.cfg = Config(sample_rate, block_size, channels, bits, 1 if stereo_decorrelation else 0,
+                          max_rice_part_order, max_rice_param, 0)
+        self.channels, self.bits, self.sample_rate, self.block_size = channels, bits, sample_rate, block_size
+        self.bytes_per_sample = bits // 8
+        self.max_frames = max_frames
+        h = ctypes.c_void_p()
+        _check(self.lib.flacgpu_open(device, ctypes.byref(self.cfg), max_frames, ctypes.byref(h)), "open")
+        self.ctx = h
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self.lib.flacgpu_close(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- bounds
+    def frame_bound(self) -> int:
+        return self.lib.flacgpu_frame_bound_bytes(ctypes.byref(self.cfg))
+
+    def reference_max_frame_bytes(self) -> int:
+        return self.lib.flacgpu_reference_max_frame_bytes(ctypes.byref(self.cfg))
+
+    # ---- encode
+    def encode_frames(self, pcm: bytes, first_frame: int = 0):
+        """Encode interleaved LE PCM -> (frame bytes, [per-frame sizes])."""
+        per = self.channels * self.bytes_per_sample
+        assert len(pcm) % per == 0
+        n = len(pcm) // per
+        nf = (n + self.block_size - 1) // self.block_size
+        cap = nf * self.frame_bound() + 64
+        out = ctypes.create_string_buffer(cap)
+        sizes = (ctypes.c_uint32 * max(nf, 1))()
+        out_len = ctypes.c_size_t(0)
+        src = ctypes.create_string_buffer(bytes(pcm), len(pcm)) if pcm else None
+        _check(self.lib.flacgpu_encode_frames(self.ctx, src, self.bytes_per_sample, n, first_frame, out, cap,
+                                              ctypes.byref(out_len), sizes), "encode_frames")
+        return out.raw[: out_len.value], list(sizes)[:nf]
+
+    def write_frame(self, planes, frame_number: int) -> bytes:
+        """Encoder.writeFrame: planar int32 samples (C x n) -> one frame."""
+        import numpy as np
+
+        planes = np.ascontiguousarray(np.asarray(planes, dtype=np.int32))
+        C, n = planes.shape
+        assert C == self.channels
+        ptrs = (ctypes.c_void_p * 8)()
+        for c in range(C):
+            ptrs[c] = planes[c].ctypes.data
+        cap = self.frame_bound() + 64
+        out = ctypes.create_string_buffer(cap)
+        fb = ctypes.c_uint32(0)
+        _check(self.lib.flacgpu_encode_frame_planar(self.ctx, ptrs, n, frame_number, out, cap, ctypes.byref(fb)),
+               "encode_frame_planar")
+        return out.raw[: fb.value]
+
+    # ---- MD5 (md5.zig) on the GPU
+    def md5(self, data: bytes) -> bytes:
+        _check(self.lib.flacgpu_md5_init(self.ctx), "md5_init")
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        _check(self.lib.flacgpu_md5_update(self.ctx, buf, len(data)), "md5_update")
+        d = ctypes.create_string_buffer(16)
+        _check(self.lib.flacgpu_md5_final(self.ctx, d), "md5_final")
+        return d.raw
+
+    def md5_update(self, data: bytes) -> None:
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        _check(self.lib.flacgpu_md5_update(self.ctx, buf, len(data)), "md5_update")
+
+    def md5_final(self) -> bytes:
+        d = ctypes.create_string_buffer(16)
+        _check(self.lib.flacgpu_md5_final(self.ctx, d), "md5_final")
+        return d.raw
+
+    # ---- device-resident batches
+    def plan(self, offsets: Sequence[int], samples: Sequence[int]) -> Plan:
+        return Plan(self, offsets, samples)
+
+    def encode_plan_device(self, plan: Plan, d_pcm: int, d_out: int, out_cap: int, d_frame_bytes: int,
+                           d_frame_offsets: int, d_total: int, d_md5: Optional[int] = None,
+                           stream: Optional[int] = None) -> None:
+        _check(self.lib.flacgpu_encode_plan_device(self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes,
+                                                   d_frame_offsets, d_total, d_md5 or None, stream or None),
+               "encode_plan_device")
+
+    # ---- instrumentation
+    def set_timing(self, on: bool) -> None:
+        _check(self.lib.flacgpu_set_timing(self.ctx, 1 if on else 0), "set_timing")
+
+    def reset_timing(self) -> None:
+        _check(self.lib.flacgpu_reset_timing(self.ctx), "reset_timing")
+
+    def kernel_time(self, k: int):
+        n = ctypes.c_uint64(0)
+        ms = ctypes.c_double(0)
+        _check(self.lib.flacgpu_kernel_time(self.ctx, k, ctypes.byref(n), ctypes.byref(ms)), "kernel_time")
+        return n.value, ms.value
+
+    def set_records(self, on: bool) -> None:
+        _check(self.lib.flacgpu_set_records(self.ctx, 1 if on else 0), "set_records")
+
+    def records(self) -> list:
+        n = ctypes.c_uint64(0)
+        _check(self.lib.flacgpu_get_records(self.ctx, None, 0, ctypes.byref(n)), "get_records")
+        arr = (FrameRecord * max(n.value, 1))()
+        _check(self.lib.flacgpu_get_records(self.ctx, arr, n.value, ctypes.byref(n)), "get_records")
+        return list(arr)[: n.value]
