@@ -1,0 +1,85 @@
+"""The C-ABI library: loads, exports every symbol include/flacgpu.h declares,
+validates configs, and refuses to run without a gfx950 device (no CPU fallback).
+No compute calls here (CPU-only container)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import flacgpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "flacgpu.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(flacgpu_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = flacgpu.load_library()
+    declared = header_functions()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in flacgpu.h but not exported"
+    assert sorted(flacgpu.exported_symbols()) == declared
+
+
+def test_abi_version():
+    assert flacgpu.load_library().flacgpu_abi_version() == 1
+
+
+def test_config_default_matches_reference():
+    c = flacgpu.load_library().flacgpu_config_default(2, 16, 44100)
+    # Config.default (encoder.zig:642-655)
+    assert (c.block_size, c.stereo_decorrelation, c.max_rice_part_order, c.max_rice_param, c.prediction) == \
+        (4096, 1, 8, 30, 0)
+
+
+def test_reference_max_frame_bytes():
+    import oracle_ref
+
+    lib = flacgpu.load_library()
+    for ch, bits in [(1, 16), (2, 16), (2, 24), (2, 32), (8, 24), (3, 8)]:
+        cfg = flacgpu.Config.default(ch, bits, 44100)
+        assert lib.flacgpu_reference_max_frame_bytes(ctypes.byref(cfg)) == \
+            oracle_ref.lib().oracle_max_frame_bytes(4096, bits, ch)
+        # the GPU slot bound is tighter than the reference buffer but never below what a frame can take
+        assert lib.flacgpu_frame_bound_bytes(ctypes.byref(cfg)) <= lib.flacgpu_reference_max_frame_bytes(
+            ctypes.byref(cfg))
+
+
+@pytest.mark.parametrize("field,value", [("bits_per_sample", 12), ("bits_per_sample", 20), ("channels", 0),
+                                         ("channels", 9), ("block_size", 0), ("block_size", 8192),
+                                         ("max_rice_part_order", 9), ("max_rice_param", 0), ("max_rice_param", 31),
+                                         ("prediction", 8), ("sample_rate", 1 << 20)])
+def test_invalid_configs_rejected(field, value):
+    lib = flacgpu.load_library()
+    cfg = flacgpu.Config.default(2, 16, 44100)
+    setattr(cfg, field, value)
+    h = ctypes.c_void_p()
+    rc = lib.flacgpu_open(0, ctypes.byref(cfg), 16, ctypes.byref(h))
+    assert rc == -1 and not h.value
+
+
+def _has_gpu():
+    try:
+        import torch
+
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-device failure path")
+def test_fails_loudly_without_device():
+    with pytest.raises(flacgpu.FlacGpuError) as e:
+        flacgpu.Encoder(2, 16, 44100)
+    assert e.value.code == -5
+
+
+def test_strerror():
+    lib = flacgpu.load_library()
+    assert lib.flacgpu_strerror(-5).decode().startswith("HIP device error")
