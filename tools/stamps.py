@@ -1,0 +1,37 @@
+"""Phase breakdown of the encode kernel from a -DFG_STAMPS build (diagnostic only)."""
+import ctypes, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "zig-flac_amd"))
+import numpy as np, torch
+import flacgpu, synth
+
+NAMES = ["stage wait", "sample load", "waste+eq", "bestOrder", "rice pass", "param search", "rec+zero barriers",
+         "hdr+passA+bar", "sub offsets", "pass B", "bar after B", "CRC+final", "copy+rec+bar"]
+S, F = 1024, 32
+enc = flacgpu.Encoder(2, 16, 44100, max_frames=S * F)
+L = enc.lib
+L.flacgpu_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+pool = synth.synth_samples(4096 * 256, 2, 16, 44100)
+pcm = np.frombuffer(synth.to_pcm_bytes(pool, 16), dtype=np.uint8)
+buf = np.concatenate([pcm[(s % 8) * 4096 * 4 * 16:][: F * 4096 * 4] for s in range(S)])
+plan = enc.plan([s * F * 4096 * 4 for s in range(S)], [F * 4096] * S)
+d_pcm = torch.from_numpy(buf).cuda()
+d_out = torch.empty(int(plan.out_bound), dtype=torch.uint8, device="cuda")
+d_fb = torch.empty(plan.n_frames, dtype=torch.int32, device="cuda")
+d_off = torch.empty(plan.n_frames, dtype=torch.int64, device="cuda")
+d_tot = torch.zeros(2, dtype=torch.int64, device="cuda")
+st = torch.cuda.current_stream()
+run = lambda: enc.encode_plan_device(plan, d_pcm.data_ptr(), d_out.data_ptr(), int(plan.out_bound), d_fb.data_ptr(),
+                                     d_off.data_ptr(), d_tot.data_ptr(), None, st.cuda_stream)
+run(); torch.cuda.synchronize()
+out = (ctypes.c_uint64 * 32)()
+print("stamps supported:", L.flacgpu_debug_stamps(enc.ctx, out, 1) == 0)
+enc.set_timing(True)
+for _ in range(5):
+    run()
+torch.cuda.synchronize()
+print("encode ms/launch", enc.kernel_time(0))
+L.flacgpu_debug_stamps(enc.ctx, out, 0)
+tot = sum(out[:13])
+for i, n in enumerate(NAMES):
+    print(f"{i:2d} {n:20s} {out[i] / max(tot,1) * 100:6.2f}%  {out[i] / (5 * S * F * 4):10.1f} clk/wave-frame")

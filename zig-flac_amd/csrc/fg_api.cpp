@@ -68,6 +68,7 @@ struct flacgpu_ctx {
     uint32_t max_frames = 0;
     uint32_t C = 0, B = 0, bits = 0, stereo = 0, nt = 0;
     uint32_t image_bytes = 0, slot_bytes = 0, lds = 0, lds_tail = 0, crc_seg = 0;
+    bool stage_separate = false;
     hipStream_t stream = nullptr, aux = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr;
@@ -81,6 +82,7 @@ struct flacgpu_ctx {
     uint8_t *d_out = nullptr;
     uint64_t out_cap = 0;
     FrameRec *d_records = nullptr;
+    unsigned long long *d_stamps = nullptr;
     bool records_on = false;
     std::vector<FrameRec> h_records;
     bool timing = false;
@@ -205,12 +207,14 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.slots = d_slots;
     a.slot_bytes = c->slot_bytes;
     a.image_bytes = c->image_bytes;
+    a.stage_separate = c->stage_separate ? 1u : 0u;
     a.frame_bytes = d_fbytes;
     a.err = c->d_err;
     a.crc_tab = c->d_crc_tab;
     a.crc_pow = c->d_crc_pow;
     a.crc_seg_words = c->crc_seg;
     a.records = c->records_on ? c->d_records : nullptr;
+    a.stamps = c->d_stamps;
     if (n_full) {
         Timed t(c, FLACGPU_K_ENCODE, st);
         a.jobs = d_jobs;
@@ -324,9 +328,11 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     c->nt = 64u * nw;
     c->image_bytes = fg_round16(frame_bound_bytes(kBlock, c->C, c->bits, c->stereo != 0));
     c->slot_bytes = (c->image_bytes + 16u + 255u) & ~255u;
-    c->lds = lds_layout(c->C, c->B, nw, c->image_bytes, true).total;
-    c->lds_tail = lds_layout(c->C, c->B, nw, c->image_bytes, false).total;
+    c->stage_separate = lds_layout(c->C, c->B, nw, c->image_bytes, true, true).total <= 160u * 1024u;
+    c->lds = lds_layout(c->C, c->B, nw, c->image_bytes, true, c->stage_separate).total;
+    c->lds_tail = lds_layout(c->C, c->B, nw, c->image_bytes, false, false).total;
     c->crc_seg = (c->image_bytes / 4u + c->nt - 1u) / c->nt;
+    c->crc_seg += c->crc_seg & 1u;  // two interleaved halves per thread
     if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u) {
         delete c;
         return FLACGPU_ERR_INVALID_CONFIG;
@@ -346,19 +352,21 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     const uint32_t ze[4] = {crc_zpow(40), crc_zpow(32), crc_zpow(24), crc_zpow(16)};
     for (int t = 0; t < 4; t++)
         for (uint32_t x = 0; x < 256; x++) tab[t * 256 + x] = (uint16_t)crc_mulmod_host(x, ze[t]);
-    std::vector<uint16_t> pw(c->nt);
+    std::vector<uint16_t> pw(c->nt + 1);
     for (uint32_t t = 0; t < c->nt; t++) pw[t] = (uint16_t)crc_zpow(32ull * c->crc_seg * (c->nt - 1u - t));
+    pw[c->nt] = (uint16_t)crc_zpow(16ull * c->crc_seg);
 
     const uint64_t F = c->max_frames;
     c->pcm_cap = F * (uint64_t)kBlock * c->C * c->B + 64;
     c->out_cap = F * (uint64_t)c->slot_bytes;
-    if (hipMalloc(&c->d_crc_tab, 1024 * 2) || hipMalloc(&c->d_crc_pow, c->nt * 2) || hipMalloc(&c->d_err, 16) ||
+    if (hipMalloc(&c->d_crc_tab, 1024 * 2) || hipMalloc(&c->d_crc_pow, (c->nt + 1) * 2) || hipMalloc(&c->d_err, 16) ||
         hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_slots, F * (uint64_t)c->slot_bytes) ||
         hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
-        hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16))
+        hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16) || hipMalloc(&c->d_stamps, 32 * 8))
         return fail(FLACGPU_ERR_OUT_OF_MEMORY);
     if (hipMemcpy(c->d_crc_tab, tab.data(), 2048, hipMemcpyHostToDevice) ||
-        hipMemcpy(c->d_crc_pow, pw.data(), c->nt * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16))
+        hipMemcpy(c->d_crc_pow, pw.data(), (c->nt + 1) * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) ||
+        hipMemset(c->d_stamps, 0, 32 * 8))
         return fail(FLACGPU_ERR_DEVICE);
     flacgpu_md5_init(c);
     *out = c;
@@ -382,6 +390,7 @@ void flacgpu_close(flacgpu_ctx *c) {
     hipFree(c->d_pcm);
     hipFree(c->d_out);
     hipFree(c->d_records);
+    hipFree(c->d_stamps);
     hipFree(c->d_md5_state);
     hipFree(c->d_md5_blocks);
     if (c->fork) hipEventDestroy(c->fork);
@@ -681,6 +690,15 @@ int flacgpu_get_records(flacgpu_ctx *c, flacgpu_frame_record *out, uint64_t max_
     const uint64_t n = std::min<uint64_t>(max_frames, c->h_records.size());
     if (out && n) std::memcpy(out, c->h_records.data(), n * sizeof(FrameRec));
     *n_frames = c->h_records.size();
+    return FLACGPU_OK;
+}
+
+// Diagnostic build only (-DFG_STAMPS): per-phase shader-clock sums of the encode kernel.
+int flacgpu_debug_stamps(flacgpu_ctx *c, uint64_t *out32, int reset) {
+    if (!c || !out32) return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(out32, c->d_stamps, 32 * 8, hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(hipMemset(c->d_stamps, 0, 32 * 8));
     return FLACGPU_OK;
 }
 

@@ -59,12 +59,14 @@ struct EncodeArgs {
     uint8_t *slots;             // frame slots, slot_bytes each
     uint32_t slot_bytes;
     uint32_t image_bytes;       // LDS frame-image bytes (multiple of 16, >= bound)
+    uint32_t stage_separate;    // full-frame kernel: staging region separate from the image (DMA prefetch)
     uint32_t *frame_bytes;      // [slot]
     uint32_t *err;              // device error word (0 = ok)
     const uint16_t *crc_tab;    // 4 x 256: z^40, z^32, z^24, z^16 byte tables (CRC-16/UMTS)
-    const uint16_t *crc_pow;    // [threads]: z^(32*seg_words*(T-1-t)) mod P
-    uint32_t crc_seg_words;     // words per thread in the CRC fold
+    const uint16_t *crc_pow;    // [threads+1]: z^(32*seg_words*(T-1-t)) mod P; [threads] = z^(16*seg_words)
+    uint32_t crc_seg_words;     // words per thread in the CRC fold (even)
     FrameRec *records;          // optional decision records [slot]
+    unsigned long long *stamps; // diagnostic builds (-DFG_STAMPS): per-phase clock sums
 };
 
 }  // namespace fg

@@ -1,0 +1,1283 @@
+// fg_device.hpp -- device helpers and the frame-encode kernel template (gfx950).
+//
+// One workgroup encodes one frame at a time (persistent loop over frames);
+// one 64-lane wave owns one candidate subframe (stereo: L, R, M, S; otherwise
+// one wave per channel) and each lane owns 64 consecutive samples held in
+// VGPRs.  The kernel restates toastori/zig-flac's Encoder.writeFrame
+// (src/lib/encoder.zig:234-284): mid/side (encoder.zig:329-350), wasted bits
+// (:556-570), subframe choice (:482-554), fixed-order analysis and residuals
+// (fixed.zig:30-201), Rice partition/parameter search (rice.zig:87-107,
+// 248-405), bit packing (frame_writer.zig:40-372) and CRC-8/CRC-16
+// (frame_writer.zig:128-148, crc16.zig).  No MFMA: there is no dense
+// contraction on this path.  Cross-lane work uses DPP (row = 16 lanes) and
+// v_readlane, never LDS permutes.  Instantiated per sample width in
+// fg_enc_b{1,2,3,4}.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#ifndef FG_NARROW
+#define FG_NARROW 0
+#endif
+#ifndef FG_WRITER_ATOMIC
+#define FG_WRITER_ATOMIC 0
+#endif
+
+#include <type_traits>
+
+#include "fg_common.hpp"
+#include "fg_layout.hpp"
+
+namespace fg {
+
+// ------------------------------------------------------------------------
+// wave64 helpers
+// ------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// v_sad_u32: |a - b| (unsigned) + acc
+__device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t acc) {
+    uint32_t d;
+    asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(acc));
+    return d;
+}
+
+enum : int {
+    DPP_XOR1 = 0xB1,     // quad_perm [1,0,3,2]
+    DPP_XOR2 = 0x4E,     // quad_perm [2,3,0,1]
+    DPP_SHR1 = 0x111,    // row_shr:1
+    DPP_SHR2 = 0x112,
+    DPP_SHR4 = 0x114,
+    DPP_SHR8 = 0x118,
+    DPP_WSHR1 = 0x138,   // wave_shr:1
+    DPP_MIRROR = 0x140,  // row_mirror
+    DPP_HMIRROR = 0x141, // row_half_mirror
+    DPP_BCAST15 = 0x142, // row_bcast:15
+    DPP_BCAST31 = 0x143, // row_bcast:31
+};
+
+// lanes whose DPP source is invalid (or whose row is masked off) read 0
+template <int CTRL, int RM = 0xF, int BM = 0xF, bool BC = true>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, BM, BC);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    return (uint64_t)dpp<CTRL>((uint32_t)v) | ((uint64_t)dpp<CTRL>((uint32_t)(v >> 32)) << 32);
+}
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
+    return (uint64_t)rdl((uint32_t)v, lane) | ((uint64_t)rdl((uint32_t)(v >> 32), lane) << 32);
+}
+
+// Row (16-lane) reductions: after the 4 steps every lane holds its row's result.
+// The intermediate steps are the lane-group results for groups of 2, 4, 8 lanes.
+template <typename T>
+__device__ __forceinline__ T dppT(T v, int which);
+#define FG_ROW_REDUCE(NAME, T, OP, DPPF)                       \
+    __device__ __forceinline__ T NAME(T v) {                   \
+        v = OP(v, DPPF<DPP_XOR1>(v));                          \
+        v = OP(v, DPPF<DPP_XOR2>(v));                          \
+        v = OP(v, DPPF<DPP_HMIRROR>(v));                       \
+        v = OP(v, DPPF<DPP_MIRROR>(v));                        \
+        return v;                                              \
+    }
+#define FG_ADD(a, b) ((a) + (b))
+#define FG_OR(a, b) ((a) | (b))
+#define FG_XOR(a, b) ((a) ^ (b))
+#define FG_MAX(a, b) ((a) > (b) ? (a) : (b))
+FG_ROW_REDUCE(row_sum32, uint32_t, FG_ADD, dpp)
+FG_ROW_REDUCE(row_sum64, uint64_t, FG_ADD, dpp64)
+FG_ROW_REDUCE(row_or32, uint32_t, FG_OR, dpp)
+FG_ROW_REDUCE(row_or64, uint64_t, FG_OR, dpp64)
+FG_ROW_REDUCE(row_xor32, uint32_t, FG_XOR, dpp)
+FG_ROW_REDUCE(row_max32, uint32_t, FG_MAX, dpp)
+
+// wave-uniform results (SGPR) from the four row results
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+    v = row_sum32(v);
+    return rdl(v, 0) + rdl(v, 16) + rdl(v, 32) + rdl(v, 48);
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+    v = row_sum64(v);
+    return rdl64(v, 0) + rdl64(v, 16) + rdl64(v, 32) + rdl64(v, 48);
+}
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
+    v = row_or32(v);
+    return rdl(v, 0) | rdl(v, 16) | rdl(v, 32) | rdl(v, 48);
+}
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+    v = row_or64(v);
+    return rdl64(v, 0) | rdl64(v, 16) | rdl64(v, 32) | rdl64(v, 48);
+}
+__device__ __forceinline__ uint32_t wave_xor32(uint32_t v) {
+    v = row_xor32(v);
+    return rdl(v, 0) ^ rdl(v, 16) ^ rdl(v, 32) ^ rdl(v, 48);
+}
+// inclusive prefix sum over the wave (Hillis-Steele in rows, then row carries)
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+    x += dpp<DPP_SHR1>(x);
+    x += dpp<DPP_SHR2>(x);
+    x += dpp<DPP_SHR4>(x);
+    x += dpp<DPP_SHR8>(x);
+    x += dpp<DPP_BCAST15, 0xA, 0xF, false>(x);
+    x += dpp<DPP_BCAST31, 0xC, 0xF, false>(x);
+    return x;
+}
+// lane l gets lane l-1's value, lane 0 gets 0
+__device__ __forceinline__ uint32_t shr1_32(uint32_t v) { return dpp<DPP_WSHR1>(v); }
+__device__ __forceinline__ int32_t shr1(int32_t v) { return (int32_t)shr1_32((uint32_t)v); }
+__device__ __forceinline__ int64_t shr1(int64_t v) { return (int64_t)dpp64<DPP_WSHR1>((uint64_t)v); }
+
+__device__ __forceinline__ uint32_t bitlen32(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(x) : 0u; }
+__device__ __forceinline__ uint32_t bitlen64(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
+__device__ __forceinline__ uint32_t zigzag32(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
+
+// ------------------------------------------------------------------------
+// Rice partition decision (rice.zig:343-405) in closed form.
+// f(0) = len + 2S; f(p) = (1+p)*len + (S >> (p-1)) - floor(len/2), p >= 1.
+// f is convex in p, so the lowest argmin over 0..maxp-1 -- the
+// parameter the reference's strict "<" scan keeps -- is the first p whose
+// forward difference is >= 0:  p = 0 if S <= ceil(len/2), else p = m + 1 for
+// the smallest m with (S >> m) <= 2*len, clamped to maxp - 1.  The escape
+// code (5 + width*len, invalid above 31 bits) is the initial candidate and
+// wins ties (strict "<" on the rice side).  Returns param (0x80|width = escape).
+// ------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rice_choose(uint64_t S, uint32_t len, uint32_t width, uint32_t maxp,
+                                                uint32_t *cost) {
+    uint32_t p;
+    if (S <= (uint64_t)((len + 1u) >> 1)) {
+        p = 0;
+    } else {
+        const uint64_t two = 2ull * len;
+        uint32_t m = 0;
+        if (S > two) {
+            m = bitlen64(S) - bitlen64(two);
+            if ((S >> m) > two) m++;
+        }
+        p = m + 1u;
+    }
+    if (p > maxp - 1u) p = maxp - 1u;
+    const uint64_t f = (p == 0) ? (uint64_t)len + (S << 1)
+                                : (uint64_t)(1u + p) * len + ((S >> (p - 1u)) - (uint64_t)(len >> 1));
+    const uint64_t esc = (width <= 31u) ? 5ull + (uint64_t)width * len : ~0ull;
+    if (f < esc) {
+        *cost = (uint32_t)f;
+        return p;
+    }
+    *cost = (uint32_t)esc;
+    return 0x80u | width;
+}
+
+// CRC-16/UMTS helpers (crc16.zig; poly 0x8005, init 0).  tab = 4 x 256 u16:
+// [0] x*z^40, [1] x*z^32, [2] x*z^24, [3] x*z^16 (mod P).  W is a stream word
+// whose first byte sits in bits 31..24.
+__device__ __forceinline__ uint32_t crc_word(uint32_t crc, uint32_t W, const uint16_t *tab) {
+    const uint32_t X = W ^ (crc << 16);
+    return (uint32_t)tab[X >> 24] ^ (uint32_t)tab[256 + ((X >> 16) & 255u)] ^
+           (uint32_t)tab[512 + ((X >> 8) & 255u)] ^ (uint32_t)tab[768 + (X & 255u)];
+}
+__device__ __forceinline__ uint32_t crc_byte(uint32_t crc, uint32_t b, const uint16_t *tab) {
+    return ((crc << 8) & 0xFFFFu) ^ (uint32_t)tab[768 + (((crc >> 8) ^ b) & 255u)];
+}
+// a(z) * b(z) mod (z^16 + z^15 + z^2 + 1)
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 15; i >= 0; i--) {
+        r <<= 1;
+        r ^= (r & 0x10000u) ? 0x18005u : 0u;
+        r ^= ((a >> i) & 1u) ? b : 0u;
+    }
+    return r & 0xFFFFu;
+}
+
+// OR `len` (<= 33) bits of v at bit position pos of the big-endian word image.
+__device__ __forceinline__ void put_bits(uint32_t *img, uint32_t pos, uint64_t v, uint32_t len) {
+    if (len == 0) return;
+    const uint32_t wi = pos >> 5, o = pos & 31u;
+    const uint64_t t = v << (64u - o - len);
+    atomicOr(&img[wi], (uint32_t)(t >> 32));
+    if (o + len > 32u) atomicOr(&img[wi + 1], (uint32_t)t);
+}
+
+// Per-lane sequential bit writer over a contiguous bit segment of the image.
+// Interior words are owned by the lane and stored plainly; the segment's first
+// and last words can be shared with the neighbouring lanes and are ORed.
+struct LaneWriter {
+    uint32_t *img;
+    uint32_t wpos;  // word holding the next bit
+    uint32_t fill;  // bits already in that word (0..31)
+    uint64_t acc;   // pending bits, left aligned
+    bool first;
+    __device__ __forceinline__ void init(uint32_t *im, uint32_t bitpos) {
+        img = im;
+        wpos = bitpos >> 5;
+        fill = bitpos & 31u;
+        acc = 0;
+        first = true;
+    }
+    __device__ __forceinline__ void emit() {
+        const uint32_t w = (uint32_t)(acc >> 32);
+        if (first) atomicOr(&img[wpos], w);
+        else img[wpos] = w;
+        first = false;
+        wpos++;
+        acc <<= 32;
+    }
+    // len <= 33, v < 2^len
+    __device__ __forceinline__ void put(uint64_t v, uint32_t len) {
+        acc |= v << (64u - fill - len);
+        fill += len;
+        if (fill >= 32u) {
+            emit();
+            fill -= 32u;
+            if (fill >= 32u) {  // only for 33-bit values
+                emit();
+                fill -= 32u;
+            }
+        }
+    }
+    __device__ __forceinline__ void zeros(uint32_t q) {
+        if (fill + q < 32u) {
+            fill += q;
+            return;
+        }
+        q -= 32u - fill;
+        emit();
+        acc = 0;
+        wpos += q >> 5;  // whole zero words: the image is pre-zeroed
+        fill = q & 31u;
+    }
+    __device__ __forceinline__ void finish() {
+        if (fill) atomicOr(&img[wpos], (uint32_t)(acc >> 32));
+    }
+};
+
+// Alternative writer: every field ORed into the image at its bit position.
+struct AtomicWriter {
+    uint32_t *img;
+    uint32_t pos;
+    __device__ __forceinline__ void init(uint32_t *im, uint32_t bitpos) {
+        img = im;
+        pos = bitpos;
+    }
+    __device__ __forceinline__ void put(uint64_t v, uint32_t len) {
+        put_bits(img, pos, v, len);
+        pos += len;
+    }
+    __device__ __forceinline__ void zeros(uint32_t q) { pos += q; }
+    __device__ __forceinline__ void finish() {}
+};
+
+// ------------------------------------------------------------------------
+// Frame header (frame_writer.zig:151-265) on one lane, emulating the
+// reference's 64-bit accumulator exactly (writeBits ORs its value unmasked;
+// only the uncommon-sample-rate field can overflow, frame_writer.zig:260).
+// ------------------------------------------------------------------------
+struct HdrWriter {
+    uint64_t accu = 0;
+    uint64_t w0 = 0;
+    uint32_t remain = 64;
+    uint32_t end = 0;
+    __device__ void bits(uint32_t n, uint64_t v) {
+        if (n == 0) return;
+        if (n <= remain) {
+            accu = (n == 64) ? 0 : (accu << n);
+            accu |= v;
+            remain -= n;
+        } else {
+            const uint32_t sh = n - remain;
+            accu = (remain == 64) ? 0 : (accu << remain);
+            accu |= v >> sh;
+            w0 = accu;  // end is at most 1 inside a header
+            end++;
+            accu = v;
+            remain = 64 - sh;
+        }
+    }
+};
+
+__device__ __forceinline__ uint32_t crc8_byte(uint32_t c, uint32_t b) {
+    c ^= b;
+#pragma unroll
+    for (int i = 0; i < 8; i++) c = (c & 0x80u) ? ((c << 1) ^ 0x07u) & 0xFFu : (c << 1) & 0xFFu;
+    return c;
+}
+
+// Writes the header (with its CRC-8) into the zeroed image; returns its bytes.
+__device__ __noinline__ uint32_t write_frame_header(uint32_t *img, uint64_t frame_number, uint32_t bits,
+                                                    uint32_t channel_code, uint32_t block_size,
+                                                    uint32_t sample_rate) {
+    HdrWriter h;
+    h.bits(16, 0xFFF8);
+    uint32_t unc_bs = 0;
+    const uint32_t ctz = (uint32_t)__builtin_ctz(block_size);
+    if ((block_size & (block_size - 1u)) == 0 && ctz <= 15 && ctz >= 8) {
+        h.bits(4, ctz);
+    } else if (block_size == 192) {
+        h.bits(4, 1);
+    } else if ((block_size >> ctz) == 144 && ctz <= 5 && ctz >= 2) {
+        h.bits(4, ctz);  // unreachable (odd part of 144*2^v is 9), kept for fidelity
+    } else if (block_size < 0x100) {
+        h.bits(4, 6);
+        unc_bs = 8;
+    } else {
+        h.bits(4, 7);
+        unc_bs = 16;
+    }
+    uint32_t unc_sr = 0, rc;
+    switch (sample_rate) {
+        case 0: rc = 0; break;
+        case 88200: rc = 1; break;
+        case 176400: rc = 2; break;
+        case 192000: rc = 3; break;
+        case 8000: rc = 4; break;
+        case 16000: rc = 5; break;
+        case 22050: rc = 6; break;
+        case 24000: rc = 7; break;
+        case 32000: rc = 8; break;
+        case 44100: rc = 9; break;
+        case 48000: rc = 10; break;
+        case 96000: rc = 11; break;
+        default:
+            if (sample_rate <= 255) { unc_sr = 4; rc = 12; }
+            else if (sample_rate <= 65535) { unc_sr = 1; rc = 13; }
+            else { unc_sr = 10; rc = 14; }
+    }
+    h.bits(4, rc);
+    h.bits(4, channel_code);
+    h.bits(4, bits == 8 ? 2u : bits == 16 ? 8u : bits == 24 ? 12u : 14u);
+    if (frame_number <= 0x7F) {
+        h.bits(8, frame_number);
+    } else {  // UTF-8 coded frame number (frame_writer.zig:235-251)
+        uint64_t buf = 0, num = frame_number, fbm = 0x3F;
+        uint32_t i = 0;
+        while (num > fbm) {
+            buf |= (0x80ull + (num & 0x3F)) << (8 * i);
+            i++;
+            num >>= 6;
+            fbm >>= 1;
+        }
+        buf |= ((0xFEull << (6 - i)) | num) << (8 * i);
+        const uint32_t nb = 8 * (i + 1);
+        h.bits(nb, buf & (~0ull >> (64 - nb)));
+    }
+    if (unc_bs) h.bits(unc_bs, block_size - 1u);
+    if (unc_sr == 4) h.bits(8, block_size);  // the reference writes the block size here (unmasked)
+    else if (unc_sr) h.bits(16, block_size / unc_sr);
+    // writeCrc8 (frame_writer.zig:128-141): stored word w0 (if any), then the accumulator
+    const uint32_t byte_end = 8u - h.remain / 8u;
+    const uint64_t a_al = (h.remain == 64) ? h.accu : (h.accu << h.remain);
+    const uint32_t nb = (h.end == 1 ? 8u : 0u) + byte_end;
+    uint32_t c = 0;
+    for (uint32_t q = 0; q < nb; q++) {
+        const uint64_t src = (h.end == 1 && q < 8) ? h.w0 : a_al;
+        const uint32_t qq = (h.end == 1 && q >= 8) ? q - 8 : q;
+        const uint32_t byte = (uint32_t)(src >> (56 - 8 * qq)) & 255u;
+        c = crc8_byte(c, byte);
+        atomicOr(&img[q >> 2], byte << (24 - 8 * (q & 3)));
+    }
+    atomicOr(&img[nb >> 2], c << (24 - 8 * (nb & 3)));
+    return nb + 1;
+}
+
+// ------------------------------------------------------------------------
+// Residual helpers
+// ------------------------------------------------------------------------
+template <int CLS>
+struct Cls {
+    using S = typename std::conditional<CLS == 32, int64_t, int32_t>::type;
+    using Sum = typename std::conditional<CLS == 16, uint32_t, uint64_t>::type;
+};
+
+template <int B>
+__device__ __forceinline__ int32_t ld_sample(const uint8_t *p) {
+    if constexpr (B == 1) return (int32_t)(*(const int8_t *)p);
+    else if constexpr (B == 2) return (int32_t)(*(const int16_t *)p);
+    else if constexpr (B == 3)
+        return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8)) | ((int32_t)(*(const int8_t *)(p + 2)) << 16);
+    else return *(const int32_t *)p;
+}
+
+struct CandRes {
+    uint32_t type, waste, bd, order, porder, method;
+    uint64_t est;
+    int64_t cval;
+};
+
+// residual of order K from sample x and history q1..q4 (fixed.zig:12-18 COEFF_SCALAR stencil):
+// wrapping i32 (narrow, fixed.zig:63-68) or i64 truncated to i32 (wide, fixed.zig:69-74).
+template <int K, typename ST>
+__device__ __forceinline__ ST fixed_residual(ST x, ST q1, ST q2, ST q3, ST q4) {
+    if constexpr (sizeof(ST) == 4) {
+        const uint32_t ux = (uint32_t)x, u1 = (uint32_t)q1, u2 = (uint32_t)q2, u3 = (uint32_t)q3, u4 = (uint32_t)q4;
+        uint32_t r;
+        if constexpr (K == 0) r = ux;
+        else if constexpr (K == 1) r = ux - u1;
+        else if constexpr (K == 2) r = ux - 2u * u1 + u2;
+        else if constexpr (K == 3) r = ux - 3u * u1 + 3u * u2 - u3;
+        else r = ux - 4u * u1 + 6u * u2 - 4u * u3 + u4;
+        return (ST)(int32_t)r;
+    } else {
+        int64_t r;
+        if constexpr (K == 0) r = x;
+        else if constexpr (K == 1) r = x - q1;
+        else if constexpr (K == 2) r = x - 2 * q1 + q2;
+        else if constexpr (K == 3) r = x - 3 * q1 + 3 * q2 - q3;
+        else r = x - 4 * q1 + 6 * q2 - 4 * q3 + q4;
+        return (ST)(int32_t)(uint32_t)(uint64_t)r;
+    }
+}
+
+// inverse: sample from residual and history (wrapping i32 / exact i64)
+__device__ __forceinline__ int32_t fixed_restore(uint32_t k, int32_t r, int32_t q1, int32_t q2, int32_t q3,
+                                                 int32_t q4) {
+    const uint32_t ur = (uint32_t)r, u1 = (uint32_t)q1, u2 = (uint32_t)q2, u3 = (uint32_t)q3, u4 = (uint32_t)q4;
+    uint32_t x;
+    if (k == 0) x = ur;
+    else if (k == 1) x = ur + u1;
+    else if (k == 2) x = ur + 2u * u1 - u2;
+    else if (k == 3) x = ur + 3u * u1 - 3u * u2 + u3;
+    else x = ur + 4u * u1 - 6u * u2 + 4u * u3 - u4;
+    return (int32_t)x;
+}
+__device__ __forceinline__ int64_t fixed_restore(uint32_t k, int64_t r, int64_t q1, int64_t q2, int64_t q3,
+                                                 int64_t q4) {
+    if (k == 0) return r;
+    if (k == 1) return r + q1;
+    if (k == 2) return r + 2 * q1 - q2;
+    if (k == 3) return r + 3 * q1 - 3 * q2 + q3;
+    return r + 4 * q1 - 6 * q2 + 4 * q3 - q4;
+}
+
+#ifdef FG_STAMPS
+#define STAMP(i)                                           \
+    do {                                                   \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+        ph_[i] += t_ - tprev_;                             \
+        tprev_ = t_;                                       \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
+
+// LDS-DMA one full frame into the padded staging area: each wave-instruction
+// moves <= 64 dwords of one 64-sample chunk (M0 = that chunk's LDS base).
+__device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint32_t *stg, uint32_t cw, uint32_t cst,
+                                          uint32_t wave, uint32_t NW, uint32_t l) {
+    const uint32_t *src = (const uint32_t *)(pcm + off);
+    for (uint32_t ch = wave; ch < 64u; ch += NW) {
+        for (uint32_t x0 = 0; x0 < cw; x0 += 64u) {
+            if (x0 + l < cw)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + ch * cw + x0 + l),
+                                                 (__attribute__((address_space(3))) void *)(stg + ch * cst + x0), 4,
+                                                 0, 0);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// The frame-encode kernel.
+//   B    : bytes per PCM sample (1..4, == bits/8)
+//   CLS  : 16 (bits <= 16), 24 (bits == 24) or 32 (bits == 32)
+//   FULL : every frame of the launch has n == 4096 (lane-owned partitions);
+//          otherwise any 1 <= n <= 4096 (tail frames; LDS partition tables)
+//   MAXT : 256 (<= 4 candidate waves) or 512
+//   NC   : channel count if fixed at compile time (1 or 2), 0 = runtime
+// ------------------------------------------------------------------------
+#ifndef FG_MINW
+#define FG_MINW 2
+#endif
+template <int B, int CLS, bool FULL, int MAXT, int NC>
+__global__ void __launch_bounds__(MAXT, (MAXT == 256 ? FG_MINW : 2)) k_encode(EncodeArgs a) {
+    using ST = typename Cls<CLS>::S;
+    using SumT = typename Cls<CLS>::Sum;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+    const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
+    // the wave index is wave-uniform: keep it (and everything derived from it) in SGPRs
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l = lane_id();
+    const uint32_t C = NC ? (uint32_t)NC : a.channels;
+    const uint32_t cw = 16u * C * B;           // dwords per 64-sample chunk
+    const uint32_t cst = cw + stage_pad(C, B);  // LDS chunk stride (dwords)
+    const bool sep = FULL && a.stage_separate;
+    const LdsLayout LY = lds_layout(C, B, NW, a.image_bytes, FULL, sep);
+    uint32_t *stg = (uint32_t *)(smem + LY.stage);
+    uint32_t *img = (uint32_t *)(smem + LY.img);
+    uint8_t *par = smem + LY.par + wave * 512u;
+    uint32_t *recs = (uint32_t *)(smem + LY.rec);
+    uint16_t *crct = (uint16_t *)(smem + LY.crc);
+    uint32_t *misc = (uint32_t *)(smem + LY.misc);
+    for (uint32_t i = tid; i < 1024u; i += NT) crct[i] = a.crc_tab[i];
+#ifdef FG_STAMPS
+    uint64_t ph_[16] = {};
+    uint64_t tprev_ = __builtin_amdgcn_s_memtime();
+#endif
+
+    // Persistent loop: this workgroup encodes frames blockIdx.x, +gridDim.x, ...; with a
+    // separate staging area the next frame's PCM is DMA'd in while this one is packed.
+    uint32_t jidx = blockIdx.x;
+    if (sep && jidx < a.n_jobs) stage_dma(a.pcm, a.jobs[jidx].pcm_off, stg, cw, cst, wave, NW, l);
+    for (; jidx < a.n_jobs; jidx += gridDim.x) {
+        const FrameJob job = a.jobs[jidx];
+        const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
+
+        // ---- 1. the frame's interleaved PCM in LDS (64 padded chunks of 64 samples)
+        if (sep) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            const uint32_t in_bytes = n * C * B;
+            const uint32_t *src = (const uint32_t *)(a.pcm + job.pcm_off);
+            const uint32_t nchunks = FULL ? 64u : (n + 63u) >> 6;
+            for (uint32_t ch = wave; ch < nchunks; ch += NW) {
+                for (uint32_t x = l; x < cw; x += 64) {
+                    const uint32_t wd = ch * cw + x;
+                    uint32_t v = 0;
+                    if (FULL || 4u * wd + 4u <= in_bytes) {
+                        v = src[wd];
+                    } else if (4u * wd < in_bytes) {
+                        const uint8_t *sb = (const uint8_t *)src + 4u * wd;
+                        for (uint32_t q = 0; 4u * wd + q < in_bytes; q++) v |= (uint32_t)sb[q] << (8 * q);
+                    }
+                    stg[ch * cst + x] = v;
+                }
+            }
+        }
+        __syncthreads();
+        STAMP(0);
+
+        // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
+        const bool stereo = a.stereo != 0;
+        const uint32_t cand = wave;
+        const uint32_t bd = a.bits + ((stereo && cand == 3) ? 1u : 0u);
+        ST s[64];
+        {
+            // The candidate switch is hoisted out of the sample loops so each loop is
+            // branch-free and all 64 (or 128) LDS reads issue back to back.
+            const uint32_t *lw = stg + l * cst;
+            const uint32_t kind = stereo ? cand : 0u;  // 0 plain channel, 1 R, 2 mid, 3 side
+            const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand;
+            auto fill = [&](auto getL, auto getR) {
+                if (kind <= 1) {
+#pragma unroll
+                    for (int j = 0; j < 64; j++) {
+                        int64_t x = kind == 0 && !stereo ? getL(j, chan) : getL(j, chan);
+                        if (!FULL && l * 64u + j >= n) x = 0;
+                        s[j] = (ST)x;
+                    }
+                } else if (kind == 2) {  // mid from un-shifted L/R (encoder.zig:337,347)
+#pragma unroll
+                    for (int j = 0; j < 64; j++) {
+                        int64_t x = (getL(j, 0u) + getR(j)) >> 1;
+                        if (!FULL && l * 64u + j >= n) x = 0;
+                        s[j] = (ST)x;
+                    }
+                } else {  // side; 33-bit at 32 bps (samples64, encoder.zig:338)
+#pragma unroll
+                    for (int j = 0; j < 64; j++) {
+                        int64_t x = getL(j, 0u) - getR(j);
+                        if (!FULL && l * 64u + j >= n) x = 0;
+                        s[j] = (ST)x;
+                    }
+                }
+            };
+            if constexpr (NC == 2 && B == 4) {
+                // (L,R) dword pair per sample (8-B pad: conflict-free ds_read_b64)
+                const uint2 *p2 = (const uint2 *)lw;
+                fill([&](int j, uint32_t c) -> int64_t { return (int32_t)(c ? p2[j].y : p2[j].x); },
+                     [&](int j) -> int64_t { return (int32_t)p2[j].y; });
+            } else if constexpr (NC == 2 && B == 2 && !FG_NARROW) {
+                // (L,R) packed in one dword per sample (16-B pad: conflict-free ds_read_b128)
+                const uint32_t *p1 = lw;
+                fill([&](int j, uint32_t c) -> int64_t { return c ? ((int32_t)p1[j] >> 16) : ((int32_t)(p1[j] << 16) >> 16); },
+                     [&](int j) -> int64_t { return (int32_t)p1[j] >> 16; });
+            } else {
+                const uint8_t *base = (const uint8_t *)lw;
+                const uint32_t CB = C * B;
+                fill([&](int j, uint32_t c) -> int64_t { return ld_sample<B>(base + j * CB + c * B); },
+                     [&](int j) -> int64_t { return ld_sample<B>(base + j * CB + B); });
+            }
+        }
+        __syncthreads();  // staging is free from here on
+        if (sep && jidx + gridDim.x < a.n_jobs)
+            stage_dma(a.pcm, a.jobs[jidx + gridDim.x].pcm_off, stg, cw, cst, wave, NW, l);
+        STAMP(1);
+
+        // ---- 3. wasted bits (encoder.zig:556-570)
+        CandRes R;
+        R.bd = bd;
+        R.order = R.porder = R.method = 0;
+        R.cval = 0;
+        {
+            uint64_t o;
+            if constexpr (CLS != 32) {
+                uint32_t o32 = 0;
+#pragma unroll
+                for (int j = 0; j < 64; j++) o32 |= (uint32_t)s[j];
+                o = wave_or32(o32);
+            } else {
+                uint64_t o64 = 0;
+#pragma unroll
+                for (int j = 0; j < 64; j++) o64 |= (uint64_t)s[j];
+                o = wave_or64(o64);
+            }
+            const uint32_t w = (o == 0) ? bd : (uint32_t)__builtin_ctzll(o);
+            if (w != 0 && w != bd) {
+#pragma unroll
+                for (int j = 0; j < 64; j++) s[j] >>= w;
+            }
+            R.waste = w;
+        }
+        const uint32_t bps = bd - R.waste;
+
+        // history: the 4 samples before this lane's chunk (lane 0 gets zeros; its i<k terms are masked)
+        const ST h1 = shr1(s[63]), h2 = shr1(s[62]), h3 = shr1(s[61]), h4 = shr1(s[60]);
+
+        // ---- 4. CONSTANT / VERBATIM defaults (encoder.zig:493-514)
+        bool try_fixed = false;
+        if (bps == 0) {
+            R.type = 0;
+            R.est = 0;
+        } else {
+            ST x0;
+            if constexpr (CLS != 32) x0 = (ST)rdl((uint32_t)s[0], 0);
+            else x0 = (ST)rdl64((uint64_t)s[0], 0);
+            bool eq = true;
+#pragma unroll
+            for (int j = 0; j < 64; j++) eq &= (s[j] == x0) || (!FULL && l * 64u + j >= n);
+            if (__all(eq)) {
+                R.type = 0;
+                R.est = bps;
+                R.cval = (int64_t)x0;
+            } else {
+                R.type = 1;
+                R.est = (uint64_t)n * bps;
+                try_fixed = FULL || n > 4;
+            }
+        }
+        STAMP(2);
+
+        uint32_t k = 0;
+        if (try_fixed) {
+            // ---- 5. bestOrder (fixed.zig:85-167)
+            uint64_t T[5];
+            if constexpr (CLS != 32) {
+                // biased differences b = e + 0x7FFFFFFF keep unsigned order == signed order:
+                // |e_{q+1}| = v_sad_u32(b_q, b_q[prev]) and b_{q+1} = (b_q[prev] ^ 0x7FFFFFFF) + b_q
+                const uint32_t KB = 0x7FFFFFFFu;
+                const uint32_t u1 = (uint32_t)h1, u2 = (uint32_t)h2, u3 = (uint32_t)h3, u4 = (uint32_t)h4;
+                uint32_t pb0 = u1 + KB;
+                uint32_t pb1 = (u1 - u2) + KB;
+                uint32_t pb2 = (u1 - 2u * u2 + u3) + KB;
+                uint32_t pb3 = (u1 - 3u * u2 + 3u * u3 - u4) + KB;
+                uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+                uint64_t T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
+#pragma unroll
+                for (int j = 0; j < 64; j++) {
+                    const bool valid = FULL || (l * 64u + j < n);
+                    const uint32_t b0 = (uint32_t)s[j] + KB;
+                    const uint32_t n0 = sad_u32(b0, KB, t0);
+                    const uint32_t n1 = sad_u32(b0, pb0, t1);
+                    const uint32_t b1 = (pb0 ^ KB) + b0;
+                    const uint32_t n2 = sad_u32(b1, pb1, t2);
+                    const uint32_t b2 = (pb1 ^ KB) + b1;
+                    const uint32_t n3 = sad_u32(b2, pb2, t3);
+                    const uint32_t b3 = (pb2 ^ KB) + b2;
+                    const uint32_t n4 = sad_u32(b3, pb3, t4);
+                    if (j < 4) {  // lane 0: e_q[i] for i < q does not count (fixed.zig:102-127)
+                        const bool z = (l == 0);
+                        t0 = valid ? n0 : t0;
+                        t1 = (valid && !(z && j < 1)) ? n1 : t1;
+                        t2 = (valid && !(z && j < 2)) ? n2 : t2;
+                        t3 = (valid && !(z && j < 3)) ? n3 : t3;
+                        t4 = (valid && !z) ? n4 : t4;
+                    } else if (!FULL) {
+                        t0 = valid ? n0 : t0; t1 = valid ? n1 : t1; t2 = valid ? n2 : t2;
+                        t3 = valid ? n3 : t3; t4 = valid ? n4 : t4;
+                    } else {
+                        t0 = n0; t1 = n1; t2 = n2; t3 = n3; t4 = n4;
+                    }
+                    pb0 = b0; pb1 = b1; pb2 = b2; pb3 = b3;
+                    if (CLS == 24 && (j & 7) == 7) {  // 8 terms of <= 2^28 fit in u32; widen
+                        T0 += t0; T1 += t1; T2 += t2; T3 += t3; T4 += t4;
+                        t0 = t1 = t2 = t3 = t4 = 0;
+                    }
+                }
+                if constexpr (CLS == 16) {
+                    // per lane <= 64 * 2^20: row sums (16 lanes) stay below 2^32
+                    const uint32_t r0 = row_sum32(t0), r1 = row_sum32(t1), r2 = row_sum32(t2), r3 = row_sum32(t3),
+                                   r4 = row_sum32(t4);
+#define FG_ROWS64(v) ((uint64_t)rdl(v, 0) + rdl(v, 16) + rdl(v, 32) + rdl(v, 48))
+                    T[0] = FG_ROWS64(r0); T[1] = FG_ROWS64(r1); T[2] = FG_ROWS64(r2); T[3] = FG_ROWS64(r3);
+                    T[4] = FG_ROWS64(r4);
+#undef FG_ROWS64
+                } else {
+                    T0 += t0; T1 += t1; T2 += t2; T3 += t3; T4 += t4;
+                    T[0] = wave_sum64(T0); T[1] = wave_sum64(T1); T[2] = wave_sum64(T2); T[3] = wave_sum64(T3);
+                    T[4] = wave_sum64(T4);
+                }
+            } else {
+                // wide path (i64): an order is invalid if any |e| exceeds i32 (fixed.zig:160-162);
+                // applying the check for bps' < 28 too is a no-op there, so one path serves both
+                int64_t p0 = h1, p1 = h1 - h2, p2 = h1 - 2 * h2 + h3, p3 = h1 - 3 * h2 + 3 * h3 - h4;
+                uint64_t A0 = 0, A1 = 0, A2 = 0, A3 = 0, A4 = 0, O0 = 0, O1 = 0, O2 = 0, O3 = 0, O4 = 0;
+#pragma unroll
+                for (int j = 0; j < 64; j++) {
+                    const bool valid = FULL || (l * 64u + j < n);
+                    const bool z = (l == 0);
+                    const int64_t e0 = s[j], e1 = e0 - p0, e2 = e1 - p1, e3 = e2 - p2, e4 = e3 - p3;
+                    const uint64_t a0 = (uint64_t)(e0 < 0 ? -e0 : e0), a1 = (uint64_t)(e1 < 0 ? -e1 : e1),
+                                   a2 = (uint64_t)(e2 < 0 ? -e2 : e2), a3 = (uint64_t)(e3 < 0 ? -e3 : e3),
+                                   a4 = (uint64_t)(e4 < 0 ? -e4 : e4);
+                    const bool v0 = valid, v1 = valid && !(z && j < 1), v2 = valid && !(z && j < 2),
+                               v3 = valid && !(z && j < 3), v4 = valid && !(z && j < 4);
+                    A0 += v0 ? a0 : 0; O0 |= v0 ? a0 : 0;
+                    A1 += v1 ? a1 : 0; O1 |= v1 ? a1 : 0;
+                    A2 += v2 ? a2 : 0; O2 |= v2 ? a2 : 0;
+                    A3 += v3 ? a3 : 0; O3 |= v3 ? a3 : 0;
+                    A4 += v4 ? a4 : 0; O4 |= v4 ? a4 : 0;
+                    p0 = e0; p1 = e1; p2 = e2; p3 = e3;
+                }
+                T[0] = wave_or64(O0) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A0);
+                T[1] = wave_or64(O1) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A1);
+                T[2] = wave_or64(O2) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A2);
+                T[3] = wave_or64(O3) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A3);
+                T[4] = wave_or64(O4) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A4);
+            }
+            k = 0;
+#pragma unroll
+            for (int q = 1; q < 5; q++)
+                if (T[q] < T[k]) k = q;  // first minimum (fixed.zig:164)
+            if (CLS == 32 && T[k] == ~0ull) try_fixed = false;  // null -> VERBATIM (encoder.zig:520)
+        }
+        STAMP(3);
+#ifdef FG_CUT3
+        if (l == 0) a.frame_bytes[job.slot + cand] = k + R.type + (uint32_t)s[7] + (uint32_t)s[63];
+        continue;
+#endif
+
+        if (try_fixed) {
+            // ---- 6. residuals in place, s[j] := e_k (lane 0 keeps its k warm-up samples),
+            // and the finest-level partition sums (rice.zig:288-340)
+            SumT S8[4] = {0, 0, 0, 0};
+            uint32_t O8[4] = {0, 0, 0, 0};
+            uint64_t *psum = nullptr;
+            uint32_t *pmax = nullptr;
+            uint32_t P = a.max_part_order, ps = 0;
+            if constexpr (!FULL) {
+                // caps of rice.calcParams (rice.zig:97-103).  The while-clamp only changes the
+                // reference's result where it would slice res[k..ps] with ps < k (UB there).
+                const uint32_t lim = k ? (31u - __builtin_clz(n)) - (31u - __builtin_clz(k)) : 15u;
+                const uint32_t ctzn = (uint32_t)__builtin_ctz(n);
+                if (ctzn < P) P = ctzn;
+                if (lim < P) P = lim;
+                while (P > 0 && (n >> P) < k) P--;
+                ps = n >> P;
+                psum = (uint64_t *)(smem + LY.psum) + wave * 512u;
+                pmax = (uint32_t *)(smem + LY.pmax) + wave * 512u;
+                for (uint32_t i = l; i < 512u; i += 64) {
+                    psum[i] = 0;
+                    pmax[i] = 0;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+            {
+                ST q1 = h1, q2 = h2, q3 = h3, q4 = h4;
+                auto body = [&](auto KK) {
+                    constexpr int K = decltype(KK)::value;
+#pragma unroll
+                    for (int j = 0; j < 64; j++) {
+                        const ST x = s[j];
+                        const ST r = fixed_residual<K, ST>(x, q1, q2, q3, q4);
+                        q4 = q3; q3 = q2; q2 = q1; q1 = x;
+                        const bool warm = (j < K) && (l == 0);
+                        if (!warm) s[j] = r;
+                        const uint32_t zz = zigzag32((int32_t)r);
+                        const uint32_t av = (zz >> 1) + (zz & 1u);  // |r|
+                        if constexpr (FULL) {
+                            S8[j >> 4] += warm ? 0u : av;
+                            O8[j >> 4] |= warm ? 0u : zz;
+                        } else {
+                            const uint32_t i = l * 64u + j;
+                            if (!warm && i < n) {
+                                const uint32_t pid = i / ps;
+                                atomicAdd((unsigned long long *)&psum[pid], (unsigned long long)av);
+                                atomicOr(&pmax[pid], zz);
+                            }
+                        }
+                    }
+                };
+                switch (k) {
+                    case 0: body(std::integral_constant<int, 0>()); break;
+                    case 1: body(std::integral_constant<int, 1>()); break;
+                    case 2: body(std::integral_constant<int, 2>()); break;
+                    case 3: body(std::integral_constant<int, 3>()); break;
+                    default: body(std::integral_constant<int, 4>()); break;
+                }
+            }
+            STAMP(4);
+
+            // ---- 7. parameter search for every partition order (rice.zig:248-279,343-395)
+            const uint32_t capp = bps > 16 ? 30u : 14u;
+            const uint32_t maxp = capp < a.max_param ? capp : a.max_param;
+            uint64_t tots[9];
+            uint32_t fives[9];
+            if constexpr (FULL) {
+                uint32_t W8[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) W8[q] = bitlen32(O8[q]);
+                const uint64_t S7a = (uint64_t)S8[0] + S8[1], S7b = (uint64_t)S8[2] + S8[3];
+                const uint32_t W7a = max(W8[0], W8[1]), W7b = max(W8[2], W8[3]);
+                const uint64_t S6 = S7a + S7b;
+                const uint32_t W6 = max(W7a, W7b);
+                // levels 5..2: partitions of 2/4/8/16 lanes -> DPP butterflies (every lane of the
+                // group ends up with the group value); levels 1, 0: the four row values (uniform)
+                uint64_t Sl[4];
+                uint32_t Wl[4];
+                {
+                    uint64_t Sg = S6;
+                    uint32_t Wg = W6;
+                    Sg += dpp64<DPP_XOR1>(Sg); Wg = max(Wg, dpp<DPP_XOR1>(Wg)); Sl[0] = Sg; Wl[0] = Wg;
+                    Sg += dpp64<DPP_XOR2>(Sg); Wg = max(Wg, dpp<DPP_XOR2>(Wg)); Sl[1] = Sg; Wl[1] = Wg;
+                    Sg += dpp64<DPP_HMIRROR>(Sg); Wg = max(Wg, dpp<DPP_HMIRROR>(Wg)); Sl[2] = Sg; Wl[2] = Wg;
+                    Sg += dpp64<DPP_MIRROR>(Sg); Wg = max(Wg, dpp<DPP_MIRROR>(Wg)); Sl[3] = Sg; Wl[3] = Wg;
+                }
+                const uint64_t r0 = rdl64(Sl[3], 0), r1 = rdl64(Sl[3], 16), r2 = rdl64(Sl[3], 32),
+                               r3 = rdl64(Sl[3], 48);
+                const uint32_t m0 = rdl(Wl[3], 0), m1 = rdl(Wl[3], 16), m2 = rdl(Wl[3], 32), m3 = rdl(Wl[3], 48);
+#pragma unroll
+                for (int o = 0; o < 9; o++) {
+                    if ((uint32_t)o <= P) {
+                        uint32_t cost = 0, c;
+                        bool five = false;
+                        if (o >= 6) {
+                            const int per = 1 << (o - 6);
+#pragma unroll
+                            for (int q = 0; q < per; q++) {
+                                uint64_t S;
+                                uint32_t W;
+                                if (o == 8) { S = S8[q]; W = W8[q]; }
+                                else if (o == 7) { S = q ? S7b : S7a; W = q ? W7b : W7a; }
+                                else { S = S6; W = W6; }
+                                const uint32_t j = l * per + q;
+                                const uint32_t len = (4096u >> o) - (j == 0 ? k : 0u);
+                                const uint32_t p = rice_choose(S, len, W, maxp, &c);
+                                cost += c;
+                                five |= (p < 0x80u && p > 14u);
+                                par[(1u << o) - 1u + j] = (uint8_t)p;
+                            }
+                            tots[o] = wave_sum32(cost);
+                        } else if (o >= 2) {
+                            const int g = 6 - o;  // a partition spans 2^g lanes
+                            const uint32_t j = l >> g;
+                            const bool lead = (l & ((1u << g) - 1u)) == 0;
+                            const uint32_t len = (4096u >> o) - (j == 0 ? k : 0u);
+                            const uint32_t p = rice_choose(Sl[g - 1], len, Wl[g - 1], maxp, &c);
+                            if (lead) {
+                                cost = c;
+                                five = (p < 0x80u && p > 14u);
+                                par[(1u << o) - 1u + j] = (uint8_t)p;
+                            }
+                            tots[o] = wave_sum32(cost);
+                        } else {
+                            // uniform: order 1 = rows {0,1} and {2,3}; order 0 = all rows
+                            const uint32_t len0 = (4096u >> o) - k, len1 = 4096u >> o;
+                            uint32_t c0, c1 = 0, p1 = 0;
+                            const uint32_t p0 = (o == 1) ? rice_choose(r0 + r1, len0, max(m0, m1), maxp, &c0)
+                                                         : rice_choose(r0 + r1 + r2 + r3, len0,
+                                                                       max(max(m0, m1), max(m2, m3)), maxp, &c0);
+                            if (o == 1) p1 = rice_choose(r2 + r3, len1, max(m2, m3), maxp, &c1);
+                            if (l == 0) {
+                                par[(1u << o) - 1u] = (uint8_t)p0;
+                                if (o == 1) par[2] = (uint8_t)p1;
+                            }
+                            five = (p0 < 0x80u && p0 > 14u) || (o == 1 && p1 < 0x80u && p1 > 14u);
+                            tots[o] = (uint64_t)c0 + c1;
+                        }
+                        fives[o] = (maxp > 14u && __any(five)) ? 1u : 0u;
+                    }
+                }
+            } else {
+                uint64_t *cs = psum, *ns = psum + 256;
+                uint32_t *cm = pmax, *nm = pmax + 256;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+                for (int o = 8; o >= 0; o--) {
+                    if ((uint32_t)o <= P) {
+                        const uint32_t np = 1u << o, len_full = n >> o;
+                        uint32_t cost = 0;
+                        bool five = false;
+                        for (uint32_t j = l; j < np; j += 64) {
+                            const uint32_t len = len_full - (j == 0 ? k : 0u);
+                            uint32_t c;
+                            const uint32_t p = rice_choose(cs[j], len, bitlen32(cm[j]), maxp, &c);
+                            cost += c;
+                            five |= (p < 0x80u && p > 14u);
+                            par[np - 1u + j] = (uint8_t)p;
+                        }
+                        tots[o] = wave_sum32(cost);
+                        fives[o] = (maxp > 14u && __any(five)) ? 1u : 0u;
+                        if (o > 0) {
+                            for (uint32_t j = l; j < (np >> 1); j += 64) {
+                                ns[j] = cs[2 * j] + cs[2 * j + 1];
+                                nm[j] = cm[2 * j] | cm[2 * j + 1];
+                            }
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            uint64_t *ts = cs; cs = ns; ns = ts;
+                            uint32_t *tm = cm; cm = nm; nm = tm;
+                        }
+                    }
+                }
+            }
+            uint64_t best = ~0ull;
+            uint32_t best_o = 0, best_m = 0;
+#pragma unroll
+            for (int o = 0; o < 9; o++) {
+                const uint64_t tot = tots[o] + ((uint64_t)(4u + fives[o]) << o);
+                if ((uint32_t)o <= P && tot <= best) {  // ascending, "<=": the higher order wins ties
+                    best = tot;                           // (rice.zig:271)
+                    best_o = (uint32_t)o;
+                    best_m = fives[o];
+                }
+            }
+
+            // ---- 8. FIXED iff its estimate < the verbatim estimate (encoder.zig:538)
+            if (best < R.est) {
+                R.type = 2;
+                R.est = best;
+                R.order = k;
+                R.porder = best_o;
+                R.method = best_m;
+            } else {
+                // verbatim needs the samples back: invert the residual recurrence
+                ST q1 = h1, q2 = h2, q3 = h3, q4 = h4;
+#pragma unroll
+                for (int j = 0; j < 64; j++) {
+                    const bool warm = (l == 0 && (uint32_t)j < k);
+                    const ST x = warm ? s[j] : fixed_restore(k, s[j], q1, q2, q3, q4);
+                    s[j] = x;
+                    q4 = q3; q3 = q2; q2 = q1; q1 = x;
+                }
+            }
+        }
+        STAMP(5);
+#ifdef FG_CUT5
+        if (l == 0) a.frame_bytes[job.slot + cand] = (uint32_t)R.est + R.type + R.porder + R.method + (uint32_t)s[5];
+        continue;
+#endif
+
+        // ---- 9. publish the candidate record, zero the frame image
+        if (l == 0) {
+            uint32_t *rc = recs + cand * 16u;
+            rc[0] = R.type; rc[1] = R.waste; rc[2] = R.bd; rc[3] = R.order; rc[4] = R.porder; rc[5] = R.method;
+            rc[6] = (uint32_t)R.est; rc[7] = (uint32_t)(R.est >> 32);
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < (a.image_bytes >> 4); i += NT) ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        STAMP(6);
+
+        // ---- 10. stereo decision (encoder.zig:441-452) or independent channels (:456-475)
+        uint32_t channel_code, n_out;
+        int my_slot;
+        if (stereo) {
+            uint64_t e[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) e[c] = (uint64_t)recs[c * 16 + 6] | ((uint64_t)recs[c * 16 + 7] << 32);
+            const uint64_t sum[4] = {e[0] + e[1], e[0] + e[3], e[3] + e[1], e[2] + e[3]};
+            uint32_t b = 0;
+#pragma unroll
+            for (int i = 1; i < 4; i++)
+                if (sum[i] < sum[b]) b = i;  // first minimum
+            channel_code = b == 0 ? 1u : b + 7u;
+            // written pairs (encoder.zig:263-268): LR {0,1}, LS {0,3}, SR {3,1}, MS {2,3}
+            const uint32_t c0 = (b == 0 || b == 1) ? 0u : (b == 2 ? 3u : 2u);
+            const uint32_t c1 = (b == 0 || b == 2) ? 1u : 3u;
+            my_slot = (cand == c0) ? 0 : ((cand == c1) ? 1 : -1);
+            n_out = 2;
+        } else {
+            channel_code = C - 1u;
+            n_out = C;
+            my_slot = (int)cand;
+        }
+        if (tid == 0) misc[16] = 8u * write_frame_header(img, job.number, a.bits, channel_code, n, a.sample_rate);
+
+        // ---- 11. exact subframe lengths (pass A), frame_writer.zig:269-372
+        uint32_t lane_off = 0;
+        uint32_t pq[4] = {0, 0, 0, 0};
+        const uint32_t param_len = 4u + R.method;
+        const uint32_t w = R.waste;
+        k = R.order;
+        const uint8_t *pp = par + ((1u << R.porder) - 1u);
+        if (my_slot >= 0) {
+            uint32_t seg = 0;
+            if (R.type == 0) {
+                seg = (l == 0) ? 8u + bd : 0u;
+            } else if (R.type == 1) {
+                const uint32_t cnt = FULL ? 64u : (n > l * 64u ? min(64u, n - l * 64u) : 0u);
+                seg = cnt * bps + ((l == 0) ? 8u + w : 0u);
+            } else {
+                const uint32_t o = R.porder;
+                if (l == 0) {
+                    const uint32_t p0 = pp[0];
+                    seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
+                }
+                if constexpr (FULL) {
+                    const uint32_t sh = 12u - o, psz = 4096u >> o;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) pq[q] = pp[(l * 64u + 16u * q) >> sh];
+#pragma unroll
+                    for (int j = 0; j < 64; j++) {
+                        const uint32_t p = pq[j >> 4];
+                        const bool esc = (p & 0x80u) != 0;
+                        const uint32_t i = l * 64u + j;
+                        if ((j & 15) == 0 && i != 0 && (i & (psz - 1u)) == 0) seg += param_len + (esc ? 5u : 0u);
+                        const bool warm = (j < 4) && (l == 0 && (uint32_t)j < k);
+                        const uint32_t zz = zigzag32((int32_t)s[j]);
+                        const uint32_t cl = esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
+                        seg += warm ? 0u : cl;
+                    }
+                } else {
+                    const uint32_t psz = n >> o;
+#pragma unroll
+                    for (int j = 0; j < 64; j++) {
+                        const uint32_t i = l * 64u + j;
+                        if (i < n && !(l == 0 && (uint32_t)j < k)) {
+                            const uint32_t p = pp[i / psz];
+                            const bool esc = (p & 0x80u) != 0;
+                            if (i != 0 && (i % psz) == 0) seg += param_len + (esc ? 5u : 0u);
+                            const uint32_t zz = zigzag32((int32_t)s[j]);
+                            seg += esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
+                        }
+                    }
+                }
+            }
+            const uint32_t incl = wave_incl_scan32(seg);
+            lane_off = incl - seg;
+            if (l == 63) misc[my_slot] = incl;
+        }
+        __syncthreads();
+        STAMP(7);
+
+        uint32_t total_bits = misc[16];
+        uint32_t sub_start = total_bits;
+        for (uint32_t i = 0; i < n_out; i++) {
+            if ((int)i < my_slot) sub_start += misc[i];
+            total_bits += misc[i];
+        }
+        STAMP(8);
+
+        // ---- 12. pack (pass B): each lane writes its contiguous bit segment
+        if (my_slot >= 0) {
+#if FG_WRITER_ATOMIC
+            AtomicWriter bw;
+#else
+            LaneWriter bw;
+#endif
+            bw.init(img, sub_start + lane_off);
+            if (R.type == 0) {
+                if (l == 0) {  // writeConstantSubframe: header 0x00, value << waste in bd bits, no wasted flag
+                    bw.put(0, 8);
+                    bw.put(((uint64_t)R.cval << w) & (~0ull >> (64 - bd)), bd);
+                }
+            } else {
+                const uint64_t mask = ~0ull >> (64 - bps);
+                if (l == 0) {
+                    const uint32_t hdr = (R.type == 1) ? (w ? 0x03u : 0x02u) : (((8u | k) << 1) | (w ? 1u : 0u));
+                    bw.put(hdr, 8);
+                    if (w) bw.put(1, w);
+                }
+                if (R.type == 1) {
+#pragma unroll
+                    for (int j = 0; j < 64; j++)
+                        if (FULL || l * 64u + j < n) bw.put((uint64_t)(int64_t)s[j] & mask, bps);
+                } else {
+                    const uint32_t o = R.porder;
+                    auto part_header = [&](uint32_t p) {
+                        if (p & 0x80u) {
+                            bw.put(0x0Fu | (R.method << 4), param_len);
+                            bw.put(p & 0x7Fu, 5);
+                        } else {
+                            bw.put(p, param_len);
+                        }
+                    };
+                    if (l == 0) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++)  // warm-up samples
+                            if ((uint32_t)j < k) bw.put((uint64_t)(int64_t)s[j] & mask, bps);
+                        bw.put((R.method << 4) | o, 6);
+                        part_header(pp[0]);
+                    }
+                    auto code = [&](int32_t r, uint32_t p) {
+                        if (p & 0x80u) {
+                            const uint32_t len = p & 0x7Fu;
+                            if (len) bw.put((uint64_t)(uint32_t)r & (~0ull >> (64 - len)), len);
+                        } else {
+                            const uint32_t zz = zigzag32(r);
+                            bw.zeros(zz >> p);
+                            bw.put((1u << p) | (zz & ((1u << p) - 1u)), p + 1u);
+                        }
+                    };
+                    if constexpr (FULL) {
+                        const uint32_t psz = 4096u >> o;
+#pragma unroll
+                        for (int j = 0; j < 64; j++) {
+                            const uint32_t i = l * 64u + j;
+                            if ((j & 15) == 0 && i != 0 && (i & (psz - 1u)) == 0) part_header(pq[j >> 4]);
+                            if (!((j < 4) && l == 0 && (uint32_t)j < k)) code((int32_t)s[j], pq[j >> 4]);
+                        }
+                    } else {
+                        const uint32_t psz = n >> o;
+#pragma unroll
+                        for (int j = 0; j < 64; j++) {
+                            const uint32_t i = l * 64u + j;
+                            if (i < n && !(l == 0 && (uint32_t)j < k)) {
+                                const uint32_t p = pp[i / psz];
+                                if (i != 0 && (i % psz) == 0) part_header(p);
+                                code((int32_t)s[j], p);
+                            }
+                        }
+                    }
+                }
+            }
+            bw.finish();
+        }
+        STAMP(9);
+        __syncthreads();
+        STAMP(10);
+
+        // ---- 13. CRC-16 of the frame (frame_writer.zig:111-125,144-148): the word stream is
+        // front-padded with zero words (a no-op for an init-0 CRC) to NT*SW words; thread t folds
+        // its SW words as two interleaved halves, joins them (x z^(32*SW/2)), shifts the result by
+        // z^(32*SW*(NT-1-t)) and the workgroup XOR-reduces.
+        const uint32_t Lb = (total_bits + 7u) >> 3;
+        const uint32_t W4 = Lb >> 2;
+        {
+            const uint32_t SW = a.crc_seg_words, H = SW >> 1;
+            const int32_t Z = (int32_t)(NT * SW) - (int32_t)W4;
+            uint32_t ca = 0, cb = 0;
+            const int32_t va = (int32_t)(tid * SW) - Z, vb = va + (int32_t)H;
+            for (uint32_t i = 0; i < H; i++) {
+                const int32_t ra = va + (int32_t)i, rb = vb + (int32_t)i;
+                if (ra >= 0) ca = crc_word(ca, img[ra], crct);
+                if (rb >= 0) cb = crc_word(cb, img[rb], crct);
+            }
+            const uint32_t ct = (ca ? crc_mulmod(ca, a.crc_pow[NT]) : 0u) ^ cb;
+            uint32_t contrib = ct ? crc_mulmod(ct, a.crc_pow[tid]) : 0u;
+            contrib = wave_xor32(contrib);
+            if (l == 0) misc[24 + wave] = contrib;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t crc = 0;
+            for (uint32_t i = 0; i < NW; i++) crc ^= misc[24 + i];
+            for (uint32_t b = W4 * 4u; b < Lb; b++)
+                crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+            put_bits(img, Lb * 8u, crc, 16);
+            const uint32_t fbytes = Lb + 2u;
+            if (fbytes + 16u > a.slot_bytes || fbytes > a.image_bytes) atomicOr(a.err, 1u);
+            a.frame_bytes[job.slot] = fbytes;
+            misc[17] = fbytes;
+        }
+        __syncthreads();
+        STAMP(11);
+
+        // ---- 14. frame image -> its slot (big-endian words to bytes)
+        {
+            const uint32_t fbytes = misc[17];
+            const uint32_t units = min((fbytes + 15u) >> 4, a.slot_bytes >> 4);
+            uint4 *dst = (uint4 *)(a.slots + (uint64_t)job.slot * a.slot_bytes);
+            for (uint32_t u = tid; u < units; u += NT) {
+                uint4 v = ((const uint4 *)img)[u];
+                v.x = __builtin_bswap32(v.x);
+                v.y = __builtin_bswap32(v.y);
+                v.z = __builtin_bswap32(v.z);
+                v.w = __builtin_bswap32(v.w);
+                dst[u] = v;
+            }
+        }
+
+        // ---- 15. optional decision records (parity tests)
+        if (a.records) {
+            FrameRec *fr = a.records + job.slot;
+            SubRec *sr = &fr->cand[cand];
+            if (l == 0) {
+                sr->type = (uint8_t)R.type;
+                sr->waste = (uint8_t)R.waste;
+                sr->bits = (uint8_t)R.bd;
+                sr->order = (uint8_t)R.order;
+                sr->part_order = (uint8_t)R.porder;
+                sr->method = (uint8_t)R.method;
+                sr->written = my_slot >= 0 ? 1 : 0;
+                sr->pad = 0;
+                sr->pad2 = 0;
+                sr->estimate = R.est;
+                sr->constant = R.cval;
+            }
+            const uint32_t np = 1u << R.porder;
+            for (uint32_t j = l; j < 256u; j += 64) sr->params[j] = (R.type == 2 && j < np) ? pp[j] : 0;
+            if (tid == 0) {
+                fr->channel_code = channel_code;
+                fr->n_cand = NW;
+                fr->frame_bytes = misc[17];
+                fr->pad = 0;
+            }
+        }
+        __syncthreads();  // image / params / scratch are reused by the next frame
+        STAMP(12);
+    }  // persistent frame loop
+#ifdef FG_STAMPS
+    if (l == 0 && a.stamps)
+        for (int i = 0; i < 13; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
+#endif
+}
+
+// persistent launch: grid = min(frames, resident workgroups)
+template <int B, int CLS, bool FULL, int MAXT, int NC>
+static hipError_t launch_encode_t(const EncodeArgs &a, uint32_t threads, uint32_t lds, hipStream_t st) {
+    auto k = k_encode<B, CLS, FULL, MAXT, NC>;
+    struct Occ {
+        uint32_t threads, lds;
+        int resident;
+    };
+    static Occ cache[8];
+    static int n_cache = 0, cus = 0;
+    int resident = 0;
+    for (int i = 0; i < n_cache; i++)
+        if (cache[i].threads == threads && cache[i].lds == lds) resident = cache[i].resident;
+    if (!resident) {
+        hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        int dev = 0, nb = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k, (int)threads, (size_t)lds);
+        if (e != hipSuccess) return e;
+        resident = nb > 0 ? nb : 1;
+        if (n_cache < 8) cache[n_cache++] = {threads, lds, resident};
+    }
+    uint64_t grid = a.n_jobs;
+    const uint64_t cap = (uint64_t)resident * (uint64_t)(cus > 0 ? cus : 256);
+    if (grid > cap) grid = cap;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(k, dim3((uint32_t)grid), dim3(threads), lds, st, a);
+    return hipGetLastError();
+}
+
+// NC = 2 for two channels, 1 for mono, 0 (runtime) otherwise; MAXT by wave count
+template <int B, int CLS>
+static hipError_t launch_encode_b(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st) {
+#define FG_L(NCV, MT)                                                                  \
+    return full ? launch_encode_t<B, CLS, true, MT, NCV>(a, threads, lds, st)          \
+                : launch_encode_t<B, CLS, false, MT, NCV>(a, threads, lds, st)
+    if (a.channels == 2) { FG_L(2, 256); }
+    if (a.channels == 1) { FG_L(1, 256); }
+    if (threads <= 256) { FG_L(0, 256); }
+    FG_L(0, 512);
+#undef FG_L
+}
+
+}  // namespace fg

@@ -5,34 +5,54 @@
 namespace fg {
 
 struct LdsLayout {
-    uint32_t img;    // frame image (BE 32-bit words), aliased with the PCM staging area
-    uint32_t par;    // rice params, kParamBytes per candidate wave
+    uint32_t stage;  // PCM staging: 64 padded chunks
+    uint32_t img;    // frame image (big-endian 32-bit words)
+    uint32_t par;    // rice params, 512 B per candidate wave (orders 0..8 at offset (1<<o)-1)
     uint32_t rec;    // 16 x u32 per candidate wave
     uint32_t crc;    // 4 x 256 u16 CRC tables
     uint32_t misc;   // 64 x u32 scratch (sub lengths, crc partials, header bits)
-    uint32_t psum;   // tail kernel only: 2 x 256 u64 per wave (inside region 0)
-    uint32_t pmax;   // tail kernel only: 2 x 256 u32 per wave (inside region 0)
+    uint32_t psum;   // tail kernel only: 2 x 256 u64 per wave
+    uint32_t pmax;   // tail kernel only: 2 x 256 u32 per wave
     uint32_t total;
 };
 
 __host__ __device__ inline uint32_t fg_round16(uint32_t x) { return (x + 15u) & ~15u; }
 
-// Staging: 64 chunks of (16*C*B + 1) dwords (one pad dword per 64-sample chunk
-// makes the per-lane sample reads bank-conflict free).
-__host__ __device__ inline uint32_t stage_bytes(uint32_t C, uint32_t B) { return 64u * (16u * C * B + 1u) * 4u; }
+// Staging: 64 chunks (one per lane) of 16*C*B dwords plus a pad that makes the
+// per-lane reads bank-conflict free for the read width used: 16-bit stereo reads
+// ds_read_b128 (pad 4 dwords), 32-bit stereo ds_read_b64 (pad 2), the rest read
+// one sample at a time (pad 1).
+__host__ __device__ inline uint32_t stage_pad(uint32_t C, uint32_t B) {
+    return (C == 2 && B == 2) ? 4u : ((C == 2 && B == 4) ? 2u : 1u);
+}
+__host__ __device__ inline uint32_t stage_bytes(uint32_t C, uint32_t B) {
+    return 64u * (16u * C * B + stage_pad(C, B)) * 4u;
+}
 
-// Region 0 holds, in turn: the PCM staging area, (tail kernel) the per-wave
-// partition-sum tables during analysis, then the zeroed frame image.
-__host__ __device__ inline LdsLayout lds_layout(uint32_t C, uint32_t B, uint32_t nw, uint32_t image_bytes, bool full) {
+// Full-frame kernel with `separate` staging: the staging area is its own region
+// so the next frame's PCM can land (LDS-DMA) while the current frame is packed.
+// Otherwise (tail kernel, or configs whose two regions exceed 160 KiB) one
+// region holds, in turn, the staging area, the per-wave partition tables (tail
+// kernel), then the frame image.
+__host__ __device__ inline LdsLayout lds_layout(uint32_t C, uint32_t B, uint32_t nw, uint32_t image_bytes, bool full,
+                                               bool separate) {
     LdsLayout L;
-    uint32_t r0 = stage_bytes(C, B);
-    if (image_bytes > r0) r0 = image_bytes;
-    if (!full && nw * 6144u > r0) r0 = nw * 6144u;
-    r0 = fg_round16(r0);
-    L.img = 0;
-    L.psum = 0;                       // tail kernel: 2 x 256 u64 per wave
-    L.pmax = nw * 4096u;              // tail kernel: 2 x 256 u32 per wave
-    L.par = r0;
+    uint32_t end;
+    if (full && separate) {
+        L.stage = 0;
+        L.img = fg_round16(stage_bytes(C, B));
+        L.psum = L.pmax = 0;
+        end = L.img + fg_round16(image_bytes);
+    } else {
+        uint32_t r0 = stage_bytes(C, B);
+        if (image_bytes > r0) r0 = image_bytes;
+        if (!full && nw * 6144u > r0) r0 = nw * 6144u;
+        L.stage = L.img = 0;
+        L.psum = 0;
+        L.pmax = nw * 4096u;
+        end = fg_round16(r0);
+    }
+    L.par = end;
     L.rec = L.par + nw * 512u;
     L.crc = L.rec + nw * 64u;
     L.misc = L.crc + 2048u;

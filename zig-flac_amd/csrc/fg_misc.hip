@@ -1,0 +1,270 @@
+// fg_misc.hip -- the small kernels around the frame encoder (gfx950): frame
+// table, size scan, compaction into contiguous bitstreams, MD5 (md5.zig /
+// RFC 1321) with one lane per independent stream, and the encode dispatcher.
+#include <hip/hip_runtime.h>
+
+#include "fg_common.hpp"
+
+namespace fg {
+
+__device__ __forceinline__ uint32_t lane_id_m() { return __lane_id(); }
+
+hipError_t launch_encode_b1(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_encode_b2(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_encode_b3(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_encode_b4(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+
+hipError_t launch_encode(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st) {
+    switch (a.bytes_per_sample) {
+        case 1: return launch_encode_b1(a, full, threads, lds, st);
+        case 2: return launch_encode_b2(a, full, threads, lds, st);
+        case 3: return launch_encode_b3(a, full, threads, lds, st);
+        case 4: return launch_encode_b4(a, full, threads, lds, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// ------------------------------------------------------------------------
+// frame table for one contiguous stream (wav2flac.zig:66-97)
+// ------------------------------------------------------------------------
+__global__ void k_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, uint32_t frame_stride_bytes,
+                            uint64_t first_number, uint32_t n_frames) {
+    uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n_frames) return;
+    uint64_t start = (uint64_t)f * block;
+    uint64_t rem = n_samples - start;
+    FrameJob j;
+    j.pcm_off = (uint64_t)f * frame_stride_bytes;
+    j.number = first_number + f;
+    j.n = (uint32_t)(rem < block ? rem : block);
+    j.slot = f;
+    jobs[f] = j;
+}
+
+// ------------------------------------------------------------------------
+// exclusive scan of frame sizes -> byte offsets (single workgroup, 1024 thr)
+// ------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n) {
+    __shared__ uint64_t wsum[16];
+    const uint32_t t = threadIdx.x, per = (n + 1023u) / 1024u;
+    const uint32_t b = t * per, e = min(n, b + per);
+    uint64_t acc = 0;
+    for (uint32_t i = b; i < e; i++) acc += sizes[i];
+    // block exclusive scan of acc
+    uint64_t x = acc;
+    const uint32_t l = lane_id_m(), w = t >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t y = __shfl_up(x, d);
+        if (l >= (uint32_t)d) x += y;
+    }
+    if (l == 63) wsum[w] = x;
+    __syncthreads();
+    uint64_t pre = 0;
+    for (uint32_t i = 0; i < w; i++) pre += wsum[i];
+    uint64_t run = pre + x - acc;
+    for (uint32_t i = b; i < e; i++) {
+        offsets[i] = run;
+        run += sizes[i];
+    }
+    if (t == 1023) {
+        uint64_t tot = 0;
+        for (int i = 0; i < 16; i++) tot += wsum[i];
+        *total = tot;
+    }
+}
+
+// ------------------------------------------------------------------------
+// compaction: frame slots -> contiguous byte stream
+// ------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_compact(const uint8_t *slots, uint32_t slot_bytes, const uint32_t *sizes,
+                                                 const uint64_t *offsets, uint8_t *out, uint64_t out_cap, uint32_t *err) {
+    const uint32_t f = blockIdx.x;
+    const uint64_t D = offsets[f];
+    const uint32_t len = sizes[f];
+    if (D + len > out_cap) {
+        if (threadIdx.x == 0) atomicOr(err, 2u);
+        return;
+    }
+    const uint8_t *src = slots + (uint64_t)f * slot_bytes;
+    const uint64_t E = D + len;
+    const uint64_t w0 = (D + 3) >> 2, w1 = E >> 2;  // fully covered dwords [w0, w1)
+    uint32_t *o32 = (uint32_t *)out;
+    const uint32_t *s32 = (const uint32_t *)src;
+    if (w1 > w0) {
+        const uint32_t sh = (uint32_t)((4 * w0 - D) & 3);  // source byte offset of dword w0 is 4*w0 - D
+        const uint64_t sbase = 4 * w0 - D;
+        for (uint64_t w = w0 + threadIdx.x; w < w1; w += blockDim.x) {
+            const uint64_t sb = sbase + 4 * (w - w0);
+            const uint32_t lo = s32[sb >> 2];
+            uint32_t v = lo;
+            if (sh) {
+                const uint32_t hi = s32[(sb >> 2) + 1];
+                v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            }
+            o32[w] = v;
+        }
+        if (threadIdx.x < 8) {
+            // head bytes [D, 4*w0) and tail bytes [4*w1, E)
+            uint64_t b = threadIdx.x < 4 ? D + threadIdx.x : 4 * w1 + (threadIdx.x - 4);
+            bool ok = threadIdx.x < 4 ? (b < 4 * w0) : (b < E);
+            if (ok) out[b] = src[b - D];
+        }
+    } else {
+        for (uint64_t b = D + threadIdx.x; b < E; b += blockDim.x) out[b] = src[b - D];
+    }
+}
+
+// ------------------------------------------------------------------------
+// MD5 (md5.zig / RFC 1321): one lane per independent stream
+// ------------------------------------------------------------------------
+constexpr uint32_t kMd5K[64] = {
+    0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+    0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+    0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+    0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+    0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+    0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+    0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+    0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
+
+#define MD5_STEP(F, a, b, c, d, m, k, s) a = b + rotl(a + F(b, c, d) + (m) + (k), s)
+#define MD5_F(b, c, d) (((b) & (c)) | (~(b) & (d)))
+#define MD5_G(b, c, d) (((b) & (d)) | ((c) & ~(d)))
+#define MD5_H(b, c, d) ((b) ^ (c) ^ (d))
+#define MD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
+
+__device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+        MD5_STEP(MD5_F, a, b, c, d, m[i + 0], kMd5K[i + 0], 7);
+        MD5_STEP(MD5_F, d, a, b, c, m[i + 1], kMd5K[i + 1], 12);
+        MD5_STEP(MD5_F, c, d, a, b, m[i + 2], kMd5K[i + 2], 17);
+        MD5_STEP(MD5_F, b, c, d, a, m[i + 3], kMd5K[i + 3], 22);
+    }
+#pragma unroll
+    for (int i = 16; i < 32; i += 4) {
+        MD5_STEP(MD5_G, a, b, c, d, m[(5 * i + 1) & 15], kMd5K[i + 0], 5);
+        MD5_STEP(MD5_G, d, a, b, c, m[(5 * i + 6) & 15], kMd5K[i + 1], 9);
+        MD5_STEP(MD5_G, c, d, a, b, m[(5 * i + 11) & 15], kMd5K[i + 2], 14);
+        MD5_STEP(MD5_G, b, c, d, a, m[(5 * i + 16) & 15], kMd5K[i + 3], 20);
+    }
+#pragma unroll
+    for (int i = 32; i < 48; i += 4) {
+        MD5_STEP(MD5_H, a, b, c, d, m[(3 * i + 5) & 15], kMd5K[i + 0], 4);
+        MD5_STEP(MD5_H, d, a, b, c, m[(3 * i + 8) & 15], kMd5K[i + 1], 11);
+        MD5_STEP(MD5_H, c, d, a, b, m[(3 * i + 11) & 15], kMd5K[i + 2], 16);
+        MD5_STEP(MD5_H, b, c, d, a, m[(3 * i + 14) & 15], kMd5K[i + 3], 23);
+    }
+#pragma unroll
+    for (int i = 48; i < 64; i += 4) {
+        MD5_STEP(MD5_I, a, b, c, d, m[(7 * i) & 15], kMd5K[i + 0], 6);
+        MD5_STEP(MD5_I, d, a, b, c, m[(7 * i + 7) & 15], kMd5K[i + 1], 10);
+        MD5_STEP(MD5_I, c, d, a, b, m[(7 * i + 14) & 15], kMd5K[i + 2], 15);
+        MD5_STEP(MD5_I, b, c, d, a, m[(7 * i + 21) & 15], kMd5K[i + 3], 21);
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+}
+
+// Full digest of n_streams independent byte ranges (offsets 4-byte aligned).
+__global__ void __launch_bounds__(64) k_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens,
+                                                    uint32_t n_streams, uint8_t *digests) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_streams) return;
+    const uint8_t *p = base + offs[s];
+    const uint64_t len = lens[s];
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    const uint64_t full = len >> 6;
+    const uint32_t *p32 = (const uint32_t *)p;
+    uint32_t m[16];
+    if (full) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) m[i] = p32[i];
+    }
+    for (uint64_t b = 0; b < full; b++) {
+        // prefetch the next block while this one is compressed
+        uint32_t nx[16];
+        const uint64_t nb_ = (b + 1 < full) ? b + 1 : b;
+#pragma unroll
+        for (int i = 0; i < 16; i++) nx[i] = p32[nb_ * 16 + i];
+        md5_compress(st, m);
+#pragma unroll
+        for (int i = 0; i < 16; i++) m[i] = nx[i];
+    }
+    // tail + padding (one or two blocks), assembled straight into message words
+    const uint32_t rem = (uint32_t)(len & 63);
+    const uint8_t *tp = p + full * 64;
+    const uint32_t nb = rem < 56 ? 1u : 2u;
+    const uint64_t bits = len * 8;
+    for (uint32_t b = 0; b < nb; b++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t idx = b * 64u + 4u * i + q;
+                uint32_t by = idx < rem ? tp[idx] : (idx == rem ? 0x80u : 0u);
+                if (b == nb - 1 && 4 * i + q >= 56) by = (uint32_t)(bits >> (8 * (4 * i + q - 56))) & 255u;
+                v |= by << (8 * q);
+            }
+            m[i] = v;
+        }
+        md5_compress(st, m);
+    }
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) digests[16 * s + 4 * i + j] = (uint8_t)(st[i] >> (8 * j));
+}
+
+// Streaming update of one MD5 state in device memory by whole 64-byte blocks.
+__global__ void k_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t st[4] = {state[0], state[1], state[2], state[3]};
+    for (uint64_t b = 0; b < n_blocks; b++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) m[i] = blocks[b * 16 + i];
+        md5_compress(st, m);
+    }
+    for (int i = 0; i < 4; i++) state[i] = st[i];
+}
+
+// ------------------------------------------------------------------------
+// host-side launch wrappers (called from fg_api.cpp)
+// ------------------------------------------------------------------------
+hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, uint32_t stride, uint64_t first,
+                            uint32_t n_frames, hipStream_t st) {
+    if (n_frames == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_make_jobs, dim3((n_frames + 255) / 256), dim3(256), 0, st, jobs, n_samples, block, stride,
+                       first, n_frames);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, sizes, offsets, total, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const uint8_t *slots, uint32_t slot_bytes, const uint32_t *sizes, const uint64_t *offsets,
+                          uint8_t *out, uint64_t out_cap, uint32_t *err, uint32_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_compact, dim3(n), dim3(256), 0, st, slots, slot_bytes, sizes, offsets, out, out_cap, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, uint32_t n,
+                              uint8_t *digests, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_md5_streams, dim3((n + 63) / 64), dim3(64), 0, st, base, offs, lens, n, digests);
+    return hipGetLastError();
+}
+
+hipError_t launch_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_md5_blocks, dim3(1), dim3(64), 0, st, state, blocks, n_blocks);
+    return hipGetLastError();
+}
+
+}  // namespace fg

@@ -15,7 +15,7 @@ import os
 from typing import Optional, Sequence
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libflacgpu.so")
+LIB_PATH = os.environ.get("FLACGPU_LIB", os.path.join(HERE, "build", "libflacgpu.so"))
 
 OK = 0
 ERRORS = {
