@@ -6,10 +6,11 @@ unit   : 1 sample = one interchannel sample (STREAMINFO unit, metadata.zig:24)
 
 A "step" is one pass of the hot path over one batch: every 4096-sample block
 of S independent streams (32768 blocks per GPU by default, BASELINE config 2)
-goes through the gfx950 kernels of libflacgpu.so -- mid/side, wasted bits,
-fixed-order analysis, Rice search, subframe choice, bit packing, CRC-8/16,
-compaction into one contiguous bitstream per stream -- and the MD5 of every
-stream's raw PCM is computed on the GPU concurrently.  Inputs are resident in
+goes through the gfx950 kernels of libflacgpu.so -- analysis (mid/side, wasted
+bits, fixed-order analysis, Rice search, subframe choice, exact frame sizes),
+frame-size scan, pack (bit packing, CRC-8/16, frames written at their final
+offsets: one contiguous bitstream per stream) -- and the MD5 of every stream's
+raw PCM is computed on the GPU concurrently.  Inputs are resident in
 HBM before the timed region; outputs stay in HBM.
 
 One process per GPU (torchrun for N > 1).  Streams are independent files, so
@@ -17,11 +18,12 @@ ranks shard streams with no data-path collective (weak scaling); a barrier and
 a max-over-ranks reduction bracket the timed region.
 
 The JSON line also carries:
-  roofline     -- the encode kernel's algorithmic bytes (PCM read + frame
-                  bytes written) per launch / its mean launch time, measured
-                  with HIP events on the launch stream during the timed
-                  steps, against 8 TB/s; `traffic` from the committed rocprofv3
-                  PMC profile (profiles/), else null;
+  roofline     -- the dominant kernel (analysis or pack, whichever takes
+                  longer): its algorithmic bytes per launch (analysis: PCM
+                  read; pack: PCM read + frame bytes written) / its mean launch
+                  time, measured with HIP events on the launch stream during
+                  the timed steps, against 8 TB/s; `traffic` from the
+                  committed rocprofv3 PMC profile (profiles/), else null;
   cpu_baseline -- the CPU restatement (oracle/, "port") timed on host
                   threads over a bounded sample of the same workload.
 """
@@ -138,8 +140,8 @@ def cpu_baseline(buf, offsets, samples, args):
     }
 
 
-def read_traffic(frames_per_launch):
-    """HBM bytes per encode launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json)."""
+def read_traffic(kernel, frames_per_launch):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (profiles/*pmc*.json)."""
     cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
     if not cands:
         return None
@@ -147,7 +149,7 @@ def read_traffic(frames_per_launch):
         d = json.load(open(cands[-1]))
         if d.get("frames_per_launch") != frames_per_launch:
             return None
-        return d.get("hbm_bytes_per_launch")
+        return d.get("hbm_bytes_per_launch", {}).get(kernel)
     except Exception:
         return None
 
@@ -218,17 +220,21 @@ def main():
     samples_per_rank = sum(samples)
     value = samples_per_rank * world * args.steps / elapsed / 1e6
 
-    # roofline of the dominant kernel (frame encode), from HIP events on its stream
-    n_launch, enc_ms = enc.kernel_time(flacgpu.K_ENCODE)
+    # roofline of the dominant kernel, from HIP events on its stream
     kt = {name: enc.kernel_time(k) for k, name in enumerate(flacgpu.KERNEL_NAMES)}
     fb = d_fb.cpu().numpy().astype(np.int64)
     total_bytes = int(d_tot[0].item())
     frame_in = 4096 * args.channels * (args.bits // 8)
-    n_full = int(plan.n_frames)
-    algo_bytes = n_full * frame_in + int(fb.sum())
-    avg_s = (enc_ms / max(n_launch, 1)) / 1e3
+    n_frames = int(plan.n_frames)
+    per_launch = {name: (v[1] / v[0]) / 1e3 for name, v in kt.items() if v[0]}
+    dom = "pack" if per_launch.get("pack", 0) > per_launch.get("analyze", 0) else "analyze"
+    algo_bytes = n_frames * frame_in + (int(fb.sum()) if dom == "pack" else 0)
+    n_launch = kt[dom][0]
+    avg_s = per_launch.get(dom, 0.0)
     achieved = algo_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic = read_traffic(n_full)
+    traffic = read_traffic(dom, n_frames)
+    path_s = sum(per_launch.get(k, 0.0) for k in ("analyze", "analyze_tail", "scan", "pack"))
+    path_bytes = n_frames * frame_in + int(fb.sum())
 
     # validity checks on the last step's output
     ok = bool(total_bytes == int(fb.sum()) and total_bytes > 0)
@@ -281,7 +287,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_encode (full frames)",
+                "kernel": "k_analyze (4096-sample frames)" if dom == "analyze" else "k_pack",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -290,6 +296,7 @@ def main():
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "launches": n_launch,
+                "encode_path_gbs": round(path_bytes / path_s / 1e9, 2) if path_s > 0 else None,
             },
             "kernel_ms_per_step": {k: round(v[1] / max(v[0], 1), 4) for k, v in kt.items() if v[0]},
             "output_ok": ok,

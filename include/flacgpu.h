@@ -70,7 +70,7 @@ const char *flacgpu_strerror(int code);
 int flacgpu_abi_version(void);
 
 /* maxFrameBytes (encoder.zig:583-595) of the reference, and the tight bound
- * the GPU path uses for its per-frame slots. */
+ * the GPU path uses for its per-frame LDS image. */
 size_t flacgpu_reference_max_frame_bytes(const flacgpu_config *cfg);
 size_t flacgpu_frame_bound_bytes(const flacgpu_config *cfg);
 
@@ -120,7 +120,7 @@ uint64_t flacgpu_plan_out_bound(const flacgpu_plan *plan);
 /* First frame index of stream s inside the plan's frame table. */
 uint64_t flacgpu_plan_stream_first_frame(const flacgpu_plan *plan, uint32_t s);
 
-/* Encode every frame of the plan from device PCM d_pcm into the compacted
+/* Encode every frame of the plan from device PCM d_pcm into the contiguous
  * device buffer d_out (capacity out_cap).  Per frame: d_frame_bytes[f] (u32)
  * and d_frame_offsets[f] (u64 byte offset of frame f in d_out; stream s's
  * bitstream is the contiguous range starting at its first frame's offset).
@@ -133,8 +133,9 @@ int flacgpu_encode_plan_device(flacgpu_ctx *ctx, const flacgpu_plan *plan, const
                                uint64_t *d_total, uint8_t *d_md5, void *hip_stream);
 
 /* ---- Instrumentation ---------------------------------------------------- */
-/* Kernel ids for flacgpu_kernel_time. */
-enum { FLACGPU_K_ENCODE = 0, FLACGPU_K_ENCODE_TAIL = 1, FLACGPU_K_SCAN = 2, FLACGPU_K_COMPACT = 3, FLACGPU_K_MD5 = 4,
+/* Kernel ids for flacgpu_kernel_time: frame analysis (4096-sample frames /
+ * short frames), frame-size scan, frame packing (all frames), stream MD5. */
+enum { FLACGPU_K_ANALYZE = 0, FLACGPU_K_ANALYZE_TAIL = 1, FLACGPU_K_SCAN = 2, FLACGPU_K_PACK = 3, FLACGPU_K_MD5 = 4,
        FLACGPU_K_COUNT = 5 };
 /* When enabled, every launch of kernel k is bracketed by HIP events on the
  * stream it runs on; flacgpu_kernel_time returns the number of timed launches

@@ -1,6 +1,6 @@
 // fg_api.cpp -- the C ABI of libflacgpu.so (include/flacgpu.h): device
 // memory planning, frame tables, launches and host <-> device movement for
-// the gfx950 kernels in fg_kernels.hip.  No CPU encoding path exists: every
+// the gfx950 kernels (fg_device.hpp, fg_misc.hip).  No CPU encoding path exists: every
 // encode goes through the HIP kernels, and a missing/unsupported device is an
 // error (FLACGPU_ERR_DEVICE), never a fallback.
 #include <hip/hip_runtime.h>
@@ -15,12 +15,10 @@
 #include "fg_layout.hpp"
 
 namespace fg {
-hipError_t launch_encode(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_stage(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
 hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, uint32_t stride, uint64_t first,
                             uint32_t n_frames, hipStream_t st);
 hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, hipStream_t st);
-hipError_t launch_compact(const uint8_t *slots, uint32_t slot_bytes, const uint32_t *sizes, const uint64_t *offsets,
-                          uint8_t *out, uint64_t out_cap, uint32_t *err, uint32_t n, hipStream_t st);
 hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, uint32_t n,
                               uint8_t *digests, hipStream_t st);
 hipError_t launch_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks, hipStream_t st);
@@ -66,15 +64,15 @@ struct flacgpu_ctx {
     int device = 0;
     flacgpu_config cfg{};
     uint32_t max_frames = 0;
-    uint32_t C = 0, B = 0, bits = 0, stereo = 0, nt = 0;
-    uint32_t image_bytes = 0, slot_bytes = 0, lds = 0, lds_tail = 0, crc_seg = 0;
-    bool stage_separate = false;
+    uint32_t C = 0, B = 0, bits = 0, stereo = 0, nt = 0, nt_pack = 0;
+    uint32_t image_bytes = 0, desc_stride = 0, lds = 0, lds_tail = 0, lds_pack = 0, crc_hmax = 0;
+    bool stage_dbuf = false;
     hipStream_t stream = nullptr, aux = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr;
+    uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr, *d_crc_join = nullptr;
     uint32_t *d_err = nullptr;
     FrameJob *d_jobs = nullptr;
-    uint8_t *d_slots = nullptr;
+    uint8_t *d_desc = nullptr;
     uint32_t *d_fbytes = nullptr;
     uint64_t *d_offsets = nullptr, *d_total = nullptr;
     uint8_t *d_pcm = nullptr;
@@ -108,9 +106,7 @@ struct flacgpu_plan {
     uint64_t *d_md5_offs = nullptr, *d_md5_lens = nullptr;
     std::vector<uint64_t> first_frame;
     uint64_t out_bound = 0;
-    uint8_t *d_slots = nullptr;  // per-plan slot area when larger than the context's
-    uint32_t *d_fbytes = nullptr;
-    uint64_t slots_frames = 0;
+    uint8_t *d_desc = nullptr;  // per-plan descriptor area when larger than the context's
 };
 
 namespace {
@@ -184,9 +180,10 @@ int validate(const flacgpu_config *cfg) {
 uint64_t frames_for(uint64_t n_samples, uint32_t bs) { return (n_samples + bs - 1) / bs; }
 
 // Queue the encode of n_full full frames (jobs[0..n_full)) and n_tail short ones
-// (jobs[n_full..)), then scan + compact into d_out.
+// (jobs[n_full..)): analysis (descriptors + exact sizes), scan (byte offsets),
+// pack (frames written at their offsets in d_out).
 int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, uint64_t n_full, uint64_t n_tail,
-                uint8_t *d_slots, uint32_t *d_fbytes, uint8_t *d_out, uint64_t out_cap, uint64_t *d_offsets,
+                uint8_t *d_desc, uint32_t *d_fbytes, uint8_t *d_out, uint64_t out_cap, uint64_t *d_offsets,
                 uint64_t *d_total, hipStream_t st) {
     const uint64_t n_frames = n_full + n_tail;
     if (n_frames == 0) {
@@ -204,37 +201,49 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.max_part_order = c->cfg.max_rice_part_order;
     a.max_param = c->cfg.max_rice_param;
     a.block_size = c->cfg.block_size;
-    a.slots = d_slots;
-    a.slot_bytes = c->slot_bytes;
+    a.desc = d_desc;
+    a.desc_stride = c->desc_stride;
     a.image_bytes = c->image_bytes;
-    a.stage_separate = c->stage_separate ? 1u : 0u;
+    a.stage_dbuf = c->stage_dbuf ? 1u : 0u;
     a.frame_bytes = d_fbytes;
+    a.offsets = d_offsets;
+    a.out = d_out;
+    a.out_cap = out_cap;
     a.err = c->d_err;
     a.crc_tab = c->d_crc_tab;
     a.crc_pow = c->d_crc_pow;
-    a.crc_seg_words = c->crc_seg;
+    a.crc_join = c->d_crc_join;
+    a.crc_hmax = c->crc_hmax;
     a.records = c->records_on ? c->d_records : nullptr;
     a.stamps = c->d_stamps;
     if (n_full) {
-        Timed t(c, FLACGPU_K_ENCODE, st);
+        Timed t(c, FLACGPU_K_ANALYZE, st);
         a.jobs = d_jobs;
         a.n_jobs = (uint32_t)n_full;
-        HIPCHK(launch_encode(a, true, c->nt, c->lds, st));
+        HIPCHK(launch_stage(0, a, true, c->nt, c->lds, st));
     }
     if (n_tail) {
-        Timed t(c, FLACGPU_K_ENCODE_TAIL, st);
+        Timed t(c, FLACGPU_K_ANALYZE_TAIL, st);
         a.jobs = d_jobs + n_full;
         a.n_jobs = (uint32_t)n_tail;
-        HIPCHK(launch_encode(a, false, c->nt, c->lds_tail, st));
+        HIPCHK(launch_stage(0, a, false, c->nt, c->lds_tail, st));
     }
     {
         Timed t(c, FLACGPU_K_SCAN, st);
         HIPCHK(launch_scan(d_fbytes, d_offsets, d_total, (uint32_t)n_frames, st));
     }
     {
-        Timed t(c, FLACGPU_K_COMPACT, st);
-        HIPCHK(launch_compact(d_slots, c->slot_bytes, d_fbytes, d_offsets, d_out, out_cap, c->d_err,
-                              (uint32_t)n_frames, st));
+        Timed t(c, FLACGPU_K_PACK, st);
+        if (n_full) {
+            a.jobs = d_jobs;
+            a.n_jobs = (uint32_t)n_full;
+            HIPCHK(launch_stage(1, a, true, c->nt_pack, c->lds_pack, st));
+        }
+        if (n_tail) {
+            a.jobs = d_jobs + n_full;
+            a.n_jobs = (uint32_t)n_tail;
+            HIPCHK(launch_stage(1, a, false, c->nt_pack, c->lds_pack, st));
+        }
     }
     return FLACGPU_OK;
 }
@@ -244,7 +253,7 @@ int check_device_error(flacgpu_ctx *c) {
     HIPCHK(hipMemcpy(&err, c->d_err, 4, hipMemcpyDeviceToHost));
     if (err) {
         hipMemset(c->d_err, 0, 4);
-        return (err & 2u) ? FLACGPU_ERR_OUTPUT_TOO_SMALL : FLACGPU_ERR_INTERNAL;
+        return (err & 2u) && !(err & 1u) ? FLACGPU_ERR_OUTPUT_TOO_SMALL : FLACGPU_ERR_INTERNAL;
     }
     return FLACGPU_OK;
 }
@@ -325,15 +334,18 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     c->B = c->bits / 8;
     c->stereo = (c->C == 2 && cfg->stereo_decorrelation) ? 1u : 0u;
     const uint32_t nw = c->stereo ? 4u : c->C;
+    const uint32_t n_out = c->stereo ? 2u : c->C;
     c->nt = 64u * nw;
-    c->image_bytes = fg_round16(frame_bound_bytes(kBlock, c->C, c->bits, c->stereo != 0));
-    c->slot_bytes = (c->image_bytes + 16u + 255u) & ~255u;
-    c->stage_separate = lds_layout(c->C, c->B, nw, c->image_bytes, true, true).total <= 160u * 1024u;
-    c->lds = lds_layout(c->C, c->B, nw, c->image_bytes, true, c->stage_separate).total;
-    c->lds_tail = lds_layout(c->C, c->B, nw, c->image_bytes, false, false).total;
-    c->crc_seg = (c->image_bytes / 4u + c->nt - 1u) / c->nt;
-    c->crc_seg += c->crc_seg & 1u;  // two interleaved halves per thread
-    if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u) {
+    c->nt_pack = 64u * n_out;
+    c->image_bytes = fg_round16(frame_bound_bytes(kBlock, c->C, c->bits, c->stereo != 0) + 16u);
+    c->desc_stride = desc_stride(n_out);
+    c->stage_dbuf = ana_layout(c->C, c->B, nw, true, true).total <= 160u * 1024u;
+    c->lds = ana_layout(c->C, c->B, nw, true, c->stage_dbuf).total;
+    c->lds_tail = ana_layout(c->C, c->B, nw, false, false).total;
+    c->lds_pack = pack_layout(c->C, c->B, c->image_bytes).total;
+    // CRC fold: half-segments of H words (odd), H <= ceil(image words / (2 * pack threads))
+    c->crc_hmax = ((c->image_bytes / 4u + 2u * c->nt_pack - 1u) / (2u * c->nt_pack)) | 1u;
+    if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u) {
         delete c;
         return FLACGPU_ERR_INVALID_CONFIG;
     }
@@ -352,20 +364,25 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     const uint32_t ze[4] = {crc_zpow(40), crc_zpow(32), crc_zpow(24), crc_zpow(16)};
     for (int t = 0; t < 4; t++)
         for (uint32_t x = 0; x < 256; x++) tab[t * 256 + x] = (uint16_t)crc_mulmod_host(x, ze[t]);
-    std::vector<uint16_t> pw(c->nt + 1);
-    for (uint32_t t = 0; t < c->nt; t++) pw[t] = (uint16_t)crc_zpow(32ull * c->crc_seg * (c->nt - 1u - t));
-    pw[c->nt] = (uint16_t)crc_zpow(16ull * c->crc_seg);
+    const uint32_t T = c->nt_pack, HM = c->crc_hmax;
+    std::vector<uint16_t> pw((size_t)HM * T), pj(HM);
+    for (uint32_t h = 1; h <= HM; h++) {
+        pj[h - 1] = (uint16_t)crc_zpow(32ull * h);
+        for (uint32_t t = 0; t < T; t++) pw[(size_t)(h - 1) * T + t] = (uint16_t)crc_zpow(64ull * h * (T - 1u - t));
+    }
 
     const uint64_t F = c->max_frames;
     c->pcm_cap = F * (uint64_t)kBlock * c->C * c->B + 64;
-    c->out_cap = F * (uint64_t)c->slot_bytes;
-    if (hipMalloc(&c->d_crc_tab, 1024 * 2) || hipMalloc(&c->d_crc_pow, (c->nt + 1) * 2) || hipMalloc(&c->d_err, 16) ||
-        hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_slots, F * (uint64_t)c->slot_bytes) ||
+    c->out_cap = F * (uint64_t)c->image_bytes;
+    if (hipMalloc(&c->d_crc_tab, 1024 * 2) || hipMalloc(&c->d_crc_pow, pw.size() * 2) ||
+        hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) ||
+        hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_desc, F * (uint64_t)c->desc_stride) ||
         hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
         hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16) || hipMalloc(&c->d_stamps, 32 * 8))
         return fail(FLACGPU_ERR_OUT_OF_MEMORY);
     if (hipMemcpy(c->d_crc_tab, tab.data(), 2048, hipMemcpyHostToDevice) ||
-        hipMemcpy(c->d_crc_pow, pw.data(), (c->nt + 1) * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) ||
+        hipMemcpy(c->d_crc_pow, pw.data(), pw.size() * 2, hipMemcpyHostToDevice) ||
+        hipMemcpy(c->d_crc_join, pj.data(), pj.size() * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) ||
         hipMemset(c->d_stamps, 0, 32 * 8))
         return fail(FLACGPU_ERR_DEVICE);
     flacgpu_md5_init(c);
@@ -381,9 +398,10 @@ void flacgpu_close(flacgpu_ctx *c) {
     for (auto e : c->event_pool) hipEventDestroy(e);
     hipFree(c->d_crc_tab);
     hipFree(c->d_crc_pow);
+    hipFree(c->d_crc_join);
     hipFree(c->d_err);
     hipFree(c->d_jobs);
-    hipFree(c->d_slots);
+    hipFree(c->d_desc);
     hipFree(c->d_fbytes);
     hipFree(c->d_offsets);
     hipFree(c->d_total);
@@ -427,7 +445,7 @@ int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sa
                                 c->stream));
         // frames with n == 4096 take the lane-owned-partition kernel, the rest the general one
         uint64_t n_full = (bs == (uint32_t)kBlock) ? ns / kBlock : 0;
-        int rc = encode_core(c, c->d_pcm, c->d_jobs, n_full, nf - n_full, c->d_slots, c->d_fbytes, c->d_out,
+        int rc = encode_core(c, c->d_pcm, c->d_jobs, n_full, nf - n_full, c->d_desc, c->d_fbytes, c->d_out,
                              c->out_cap, c->d_offsets, c->d_total, c->stream);
         if (rc) return rc;
         uint64_t total = 0;
@@ -580,7 +598,7 @@ int flacgpu_plan_create(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs
     p->n_frames = slot;
     p->n_full = full.size();
     p->n_tail = tail.size();
-    p->out_bound = slot * (uint64_t)c->slot_bytes;
+    p->out_bound = slot * (uint64_t)c->image_bytes;
     full.insert(full.end(), tail.begin(), tail.end());
     auto fail = [&](int code) {
         flacgpu_plan_destroy(p);
@@ -598,11 +616,8 @@ int flacgpu_plan_create(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs
             hipMemcpy(p->d_md5_lens, lens.data(), n_streams * 8, hipMemcpyHostToDevice))
             return fail(FLACGPU_ERR_DEVICE);
     }
-    if (slot > c->max_frames) {
-        if (hipMalloc(&p->d_slots, slot * (uint64_t)c->slot_bytes) || hipMalloc(&p->d_fbytes, slot * 4))
-            return fail(FLACGPU_ERR_OUT_OF_MEMORY);
-        p->slots_frames = slot;
-    }
+    if (slot > c->max_frames && hipMalloc(&p->d_desc, slot * (uint64_t)c->desc_stride))
+        return fail(FLACGPU_ERR_OUT_OF_MEMORY);
     *out = p;
     return FLACGPU_OK;
 }
@@ -612,8 +627,7 @@ void flacgpu_plan_destroy(flacgpu_plan *p) {
     hipFree(p->d_jobs);
     hipFree(p->d_md5_offs);
     hipFree(p->d_md5_lens);
-    hipFree(p->d_slots);
-    hipFree(p->d_fbytes);
+    hipFree(p->d_desc);
     delete p;
 }
 
@@ -631,7 +645,7 @@ int flacgpu_encode_plan_device(flacgpu_ctx *c, const flacgpu_plan *p, const void
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     if (c->records_on && p->n_frames > c->max_frames) return FLACGPU_ERR_INVALID_INPUT;
-    uint8_t *slots = p->d_slots ? p->d_slots : c->d_slots;
+    uint8_t *desc = p->d_desc ? p->d_desc : c->d_desc;
     // MD5 of every stream on the auxiliary stream, overlapping the encode kernels
     if (d_md5 && p->n_streams) {
         HIPCHK(hipEventRecord(c->fork, st));
@@ -643,7 +657,7 @@ int flacgpu_encode_plan_device(flacgpu_ctx *c, const flacgpu_plan *p, const void
         }
         HIPCHK(hipEventRecord(c->join, c->aux));
     }
-    int rc = encode_core(c, (const uint8_t *)d_pcm, p->d_jobs, p->n_full, p->n_tail, slots, d_frame_bytes, d_out,
+    int rc = encode_core(c, (const uint8_t *)d_pcm, p->d_jobs, p->n_full, p->n_tail, desc, d_frame_bytes, d_out,
                          out_cap, d_frame_offsets, d_total, st);
     if (rc) return rc;
     if (d_md5 && p->n_streams) HIPCHK(hipStreamWaitEvent(st, c->join, 0));

@@ -1,5 +1,6 @@
-// fg_common.hpp -- POD types shared by the HIP kernels (fg_kernels.hip) and the
-// host orchestration behind the C ABI (fg_api.cpp).  gfx950 only.
+// fg_common.hpp -- POD types shared by the HIP kernels (fg_device.hpp,
+// fg_misc.hip) and the host orchestration behind the C ABI (fg_api.cpp).
+// gfx950 only.
 #pragma once
 #include <stdint.h>
 
@@ -44,6 +45,38 @@ struct FrameRec {
     SubRec cand[8];
 };
 
+// Frame descriptor written by the analysis kernel and consumed by the pack
+// kernel: everything needed to emit the frame's bits at its final byte offset
+// without redoing the search.  Stride: desc_stride(n_out).
+struct SubDesc {
+    uint8_t type;        // 0 CONSTANT, 1 VERBATIM, 2 FIXED
+    uint8_t waste;
+    uint8_t bd;          // bits of the (side: +1) channel before the waste shift
+    uint8_t order;       // fixed predictor order
+    uint8_t porder;      // rice partition order
+    uint8_t method;      // 0 RICE, 1 RICE2
+    uint8_t cand;        // stereo: 0 L, 1 R, 2 M, 3 S; else the channel
+    uint8_t pad;
+    uint32_t bits;       // exact subframe bits
+    uint32_t pad2;
+    int64_t cval;        // CONSTANT value (after the waste shift)
+    uint32_t lane_bits[64];  // bits of lane l's 64-sample segment (pass A)
+    uint8_t params[256];     // rice params of the chosen order (0x80|w = escape)
+    uint8_t pad3[8];
+};
+static_assert(sizeof(SubDesc) == 544, "SubDesc layout");
+
+struct FrameDesc {
+    uint32_t hdr_bytes;     // frame header bytes incl. CRC-8
+    uint32_t total_bits;    // header + subframes (before the byte pad)
+    uint32_t channel_code;
+    uint32_t n_out;         // subframes written
+    uint32_t hdr[4];        // header bytes as big-endian words, zero past hdr_bytes
+};
+static_assert(sizeof(FrameDesc) == 32, "FrameDesc layout");
+
+__host__ __device__ constexpr uint32_t desc_stride(uint32_t n_out) { return 32u + n_out * 544u; }
+
 struct EncodeArgs {
     const uint8_t *pcm;         // device PCM base
     const FrameJob *jobs;       // frame table
@@ -56,15 +89,19 @@ struct EncodeArgs {
     uint32_t max_part_order;    // 0..8
     uint32_t max_param;         // 1..30
     uint32_t block_size;        // stream block size (header field for short frames is n)
-    uint8_t *slots;             // frame slots, slot_bytes each
-    uint32_t slot_bytes;
-    uint32_t image_bytes;       // LDS frame-image bytes (multiple of 16, >= bound)
-    uint32_t stage_separate;    // full-frame kernel: staging region separate from the image (DMA prefetch)
-    uint32_t *frame_bytes;      // [slot]
-    uint32_t *err;              // device error word (0 = ok)
+    uint8_t *desc;              // frame descriptors [slot], desc_stride bytes each
+    uint32_t desc_stride;
+    uint32_t image_bytes;       // pack kernel LDS frame-image bytes (multiple of 16, >= bound + 16)
+    uint32_t stage_dbuf;        // full-frame analysis kernel: double-buffered staging (LDS-DMA prefetch)
+    uint32_t *frame_bytes;      // [slot] exact frame bytes (analysis kernel)
+    const uint64_t *offsets;    // [slot] byte offset of the frame in out (scan)
+    uint8_t *out;               // contiguous output bitstream
+    uint64_t out_cap;
+    uint32_t *err;              // device error word (0 = ok; bit 0 invariant, bit 1 output too small)
     const uint16_t *crc_tab;    // 4 x 256: z^40, z^32, z^24, z^16 byte tables (CRC-16/UMTS)
-    const uint16_t *crc_pow;    // [threads+1]: z^(32*seg_words*(T-1-t)) mod P; [threads] = z^(16*seg_words)
-    uint32_t crc_seg_words;     // words per thread in the CRC fold (even)
+    const uint16_t *crc_pow;    // [(H-1)*pack_threads + t] = z^(64*H*(T-1-t)) mod P, H = 1..crc_hmax
+    const uint16_t *crc_join;   // [H-1] = z^(32*H)
+    uint32_t crc_hmax;          // largest half-segment (words) of the CRC fold
     FrameRec *records;          // optional decision records [slot]
     unsigned long long *stamps; // diagnostic builds (-DFG_STAMPS): per-phase clock sums
 };

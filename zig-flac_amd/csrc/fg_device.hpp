@@ -17,9 +17,6 @@
 #ifndef FG_NARROW
 #define FG_NARROW 0
 #endif
-#ifndef FG_WRITER_ATOMIC
-#define FG_WRITER_ATOMIC 0
-#endif
 
 #include <type_traits>
 
@@ -32,6 +29,12 @@ namespace fg {
 // wave64 helpers
 // ------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+// A value the optimiser cannot see through: values derived from it are recomputed
+// where used instead of being hoisted out of the persistent loop and held in VGPRs.
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 // v_sad_u32: |a - b| (unsigned) + acc
 __device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t acc) {
@@ -201,60 +204,16 @@ __device__ __forceinline__ void put_bits(uint32_t *img, uint32_t pos, uint64_t v
     if (o + len > 32u) atomicOr(&img[wi + 1], (uint32_t)t);
 }
 
-// Per-lane sequential bit writer over a contiguous bit segment of the image.
-// Interior words are owned by the lane and stored plainly; the segment's first
-// and last words can be shared with the neighbouring lanes and are ORed.
-struct LaneWriter {
-    uint32_t *img;
-    uint32_t wpos;  // word holding the next bit
-    uint32_t fill;  // bits already in that word (0..31)
-    uint64_t acc;   // pending bits, left aligned
-    bool first;
-    __device__ __forceinline__ void init(uint32_t *im, uint32_t bitpos) {
-        img = im;
-        wpos = bitpos >> 5;
-        fill = bitpos & 31u;
-        acc = 0;
-        first = true;
-    }
-    __device__ __forceinline__ void emit() {
-        const uint32_t w = (uint32_t)(acc >> 32);
-        if (first) atomicOr(&img[wpos], w);
-        else img[wpos] = w;
-        first = false;
-        wpos++;
-        acc <<= 32;
-    }
-    // len <= 33, v < 2^len
-    __device__ __forceinline__ void put(uint64_t v, uint32_t len) {
-        acc |= v << (64u - fill - len);
-        fill += len;
-        if (fill >= 32u) {
-            emit();
-            fill -= 32u;
-            if (fill >= 32u) {  // only for 33-bit values
-                emit();
-                fill -= 32u;
-            }
-        }
-    }
-    __device__ __forceinline__ void zeros(uint32_t q) {
-        if (fill + q < 32u) {
-            fill += q;
-            return;
-        }
-        q -= 32u - fill;
-        emit();
-        acc = 0;
-        wpos += q >> 5;  // whole zero words: the image is pre-zeroed
-        fill = q & 31u;
-    }
-    __device__ __forceinline__ void finish() {
-        if (fill) atomicOr(&img[wpos], (uint32_t)(acc >> 32));
-    }
-};
+// Branch-free variant: always two ORs (the second may OR 0); len == 0 writes nothing.
+__device__ __forceinline__ void put_or2(uint32_t *img, uint32_t pos, uint64_t v, uint32_t len) {
+    const uint32_t wi = pos >> 5, o = pos & 31u;
+    const uint64_t t = len ? (v << (64u - o - len)) : 0ull;
+    atomicOr(&img[wi], (uint32_t)(t >> 32));
+    atomicOr(&img[wi + 1], (uint32_t)t);
+}
 
-// Alternative writer: every field ORed into the image at its bit position.
+// Sequential writer for the few per-subframe header fields: every field ORed into
+// the image at its bit position.
 struct AtomicWriter {
     uint32_t *img;
     uint32_t pos;
@@ -406,51 +365,6 @@ struct CandRes {
     int64_t cval;
 };
 
-// residual of order K from sample x and history q1..q4 (fixed.zig:12-18 COEFF_SCALAR stencil):
-// wrapping i32 (narrow, fixed.zig:63-68) or i64 truncated to i32 (wide, fixed.zig:69-74).
-template <int K, typename ST>
-__device__ __forceinline__ ST fixed_residual(ST x, ST q1, ST q2, ST q3, ST q4) {
-    if constexpr (sizeof(ST) == 4) {
-        const uint32_t ux = (uint32_t)x, u1 = (uint32_t)q1, u2 = (uint32_t)q2, u3 = (uint32_t)q3, u4 = (uint32_t)q4;
-        uint32_t r;
-        if constexpr (K == 0) r = ux;
-        else if constexpr (K == 1) r = ux - u1;
-        else if constexpr (K == 2) r = ux - 2u * u1 + u2;
-        else if constexpr (K == 3) r = ux - 3u * u1 + 3u * u2 - u3;
-        else r = ux - 4u * u1 + 6u * u2 - 4u * u3 + u4;
-        return (ST)(int32_t)r;
-    } else {
-        int64_t r;
-        if constexpr (K == 0) r = x;
-        else if constexpr (K == 1) r = x - q1;
-        else if constexpr (K == 2) r = x - 2 * q1 + q2;
-        else if constexpr (K == 3) r = x - 3 * q1 + 3 * q2 - q3;
-        else r = x - 4 * q1 + 6 * q2 - 4 * q3 + q4;
-        return (ST)(int32_t)(uint32_t)(uint64_t)r;
-    }
-}
-
-// inverse: sample from residual and history (wrapping i32 / exact i64)
-__device__ __forceinline__ int32_t fixed_restore(uint32_t k, int32_t r, int32_t q1, int32_t q2, int32_t q3,
-                                                 int32_t q4) {
-    const uint32_t ur = (uint32_t)r, u1 = (uint32_t)q1, u2 = (uint32_t)q2, u3 = (uint32_t)q3, u4 = (uint32_t)q4;
-    uint32_t x;
-    if (k == 0) x = ur;
-    else if (k == 1) x = ur + u1;
-    else if (k == 2) x = ur + 2u * u1 - u2;
-    else if (k == 3) x = ur + 3u * u1 - 3u * u2 + u3;
-    else x = ur + 4u * u1 - 6u * u2 + 4u * u3 - u4;
-    return (int32_t)x;
-}
-__device__ __forceinline__ int64_t fixed_restore(uint32_t k, int64_t r, int64_t q1, int64_t q2, int64_t q3,
-                                                 int64_t q4) {
-    if (k == 0) return r;
-    if (k == 1) return r + q1;
-    if (k == 2) return r + 2 * q1 - q2;
-    if (k == 3) return r + 3 * q1 - 3 * q2 + q3;
-    return r + 4 * q1 - 6 * q2 + 4 * q3 - q4;
-}
-
 #ifdef FG_STAMPS
 #define STAMP(i)                                           \
     do {                                                   \
@@ -479,131 +393,186 @@ __device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint
     }
 }
 
+
+// Stage one frame's interleaved PCM synchronously (tail frames zero-filled).
+template <bool FULL>
+__device__ __forceinline__ void stage_sync(const uint8_t *pcm, uint64_t off, uint32_t n, uint32_t CB, uint32_t *stg,
+                                           uint32_t cw, uint32_t cst, uint32_t wave, uint32_t NW, uint32_t l) {
+    const uint32_t in_bytes = n * CB;
+    const uint32_t *src = (const uint32_t *)(pcm + off);
+    const uint32_t nchunks = FULL ? 64u : (n + 63u) >> 6;
+    for (uint32_t ch = wave; ch < nchunks; ch += NW) {
+        for (uint32_t x = l; x < cw; x += 64) {
+            const uint32_t wd = ch * cw + x;
+            uint32_t v = 0;
+            if (FULL || 4u * wd + 4u <= in_bytes) {
+                v = src[wd];
+            } else if (4u * wd < in_bytes) {
+                const uint8_t *sb = (const uint8_t *)src + 4u * wd;
+                for (uint32_t q = 0; 4u * wd + q < in_bytes; q++) v |= (uint32_t)sb[q] << (8 * q);
+            }
+            stg[ch * cst + x] = v;
+        }
+    }
+}
+
+// Lane l loads samples [64l, 64l+64) of candidate `cand` from the staging area:
+// stereo 0 L, 1 R, 2 mid, 3 side (encoder.zig:329-350, from the un-shifted
+// L/R), otherwise channel `cand`.  Samples past n read as 0.  The candidate
+// switch is hoisted out of the sample loops so each loop is branch-free.
+template <int B, int CLS, bool FULL, int NC>
+__device__ __forceinline__ void load_candidate(const uint32_t *stg, uint32_t cst, uint32_t l, uint32_t n, bool stereo,
+                                               uint32_t cand, uint32_t C, typename Cls<CLS>::S (&s)[64]) {
+    using ST = typename Cls<CLS>::S;
+    const uint32_t *lw = stg + l * cst;
+    const uint32_t kind = stereo ? cand : 0u;  // 0 plain channel, 1 R, 2 mid, 3 side
+    const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand;
+    // Groups of 16 samples with a scheduling barrier between them: without it the
+    // scheduler hoists every LDS read ahead of the unpacking and holds the raw words
+    // and the samples live together (2x the registers).
+    auto fill = [&](auto getL, auto getR) {
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            if (kind <= 1) {
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    const int j = 16 * g + jj;
+                    int64_t x = getL(j, chan);
+                    if (!FULL && l * 64u + j >= n) x = 0;
+                    s[j] = (ST)x;
+                }
+            } else if (kind == 2) {  // mid (encoder.zig:337,347)
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    const int j = 16 * g + jj;
+                    int64_t x = (getL(j, 0u) + getR(j)) >> 1;
+                    if (!FULL && l * 64u + j >= n) x = 0;
+                    s[j] = (ST)x;
+                }
+            } else {  // side; 33-bit at 32 bps (samples64, encoder.zig:338)
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    const int j = 16 * g + jj;
+                    int64_t x = getL(j, 0u) - getR(j);
+                    if (!FULL && l * 64u + j >= n) x = 0;
+                    s[j] = (ST)x;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    if constexpr (NC == 2 && B == 4) {
+        // (L,R) dword pair per sample (8-B pad: conflict-free ds_read_b64)
+        const uint2 *p2 = (const uint2 *)lw;
+        fill([&](int j, uint32_t c) -> int64_t { return (int32_t)(c ? p2[j].y : p2[j].x); },
+             [&](int j) -> int64_t { return (int32_t)p2[j].y; });
+    } else if constexpr (NC == 2 && B == 2 && !FG_NARROW) {
+        // (L,R) packed in one dword per sample (16-B pad: conflict-free ds_read_b128)
+        const uint32_t *p1 = lw;
+        fill([&](int j, uint32_t c) -> int64_t { return c ? ((int32_t)p1[j] >> 16) : ((int32_t)(p1[j] << 16) >> 16); },
+             [&](int j) -> int64_t { return (int32_t)p1[j] >> 16; });
+    } else {
+        const uint8_t *base = (const uint8_t *)lw;
+        const uint32_t CB = C * B;
+        fill([&](int j, uint32_t c) -> int64_t { return ld_sample<B>(base + j * CB + c * B); },
+             [&](int j) -> int64_t { return ld_sample<B>(base + j * CB + B); });
+    }
+}
+
+// Fixed-predictor residuals in place, s[j] := e_k (lane 0 keeps its k warm-up
+// samples; history h1..h4 = the 4 samples before the lane's chunk), for a runtime
+// (wave-uniform) order k: the difference chain
+// e_{q+1}[i] = e_q[i] - e_q[i-1] for q < 4, then a uniform select.  One code
+// path instead of five keeps the register allocation of the callers compact.
+// Narrow: wrapping u32 (== the stencil mod 2^32); wide: exact i64 truncated to
+// i32 (fixed.zig:69-74).
+template <typename ST, typename F>
+__device__ __forceinline__ void residuals_generic(ST (&s)[64], ST h1, ST h2, ST h3, ST h4, uint32_t l, uint32_t k,
+                                                  F &&f) {
+    using UT = typename std::conditional<sizeof(ST) == 4, uint32_t, uint64_t>::type;
+    const UT u1 = (UT)h1, u2 = (UT)h2, u3 = (UT)h3, u4 = (UT)h4;
+    UT p0 = u1, p1 = u1 - u2, p2 = u1 - 2u * u2 + u3, p3 = u1 - 3u * u2 + 3u * u3 - u4;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const UT e0 = (UT)s[j], e1 = e0 - p0, e2 = e1 - p1, e3 = e2 - p2, e4 = e3 - p3;
+        p0 = e0; p1 = e1; p2 = e2; p3 = e3;
+        const UT e = k == 0 ? e0 : k == 1 ? e1 : k == 2 ? e2 : k == 3 ? e3 : e4;
+        const ST r = (ST)(int32_t)(uint32_t)e;
+        const bool warm = (j < 4) && (l == 0) && ((uint32_t)j < k);
+        if (!warm) s[j] = r;
+        f(j, warm, r);
+    }
+}
+
 // ------------------------------------------------------------------------
-// The frame-encode kernel.
+// Kernel 1: frame analysis.  One workgroup per frame (persistent loop), one
+// wave per candidate subframe.  Decides every candidate exactly as
+// Encoder.writeFrame does (encoder.zig:234-284, 482-570), measures the exact
+// bits of each candidate's lane segments (pass A of frame_writer.zig:269-372),
+// takes the stereo decision (encoder.zig:441-452), and writes the frame
+// descriptor + exact frame size.  No frame bytes are produced here.
 //   B    : bytes per PCM sample (1..4, == bits/8)
 //   CLS  : 16 (bits <= 16), 24 (bits == 24) or 32 (bits == 32)
-//   FULL : every frame of the launch has n == 4096 (lane-owned partitions);
-//          otherwise any 1 <= n <= 4096 (tail frames; LDS partition tables)
+//   FULL : every frame of the launch has n == 4096 (lane-owned partitions,
+//          LDS-DMA prefetch); otherwise any 1 <= n <= 4096 (tail frames)
 //   MAXT : 256 (<= 4 candidate waves) or 512
 //   NC   : channel count if fixed at compile time (1 or 2), 0 = runtime
 // ------------------------------------------------------------------------
 #ifndef FG_MINW
-#define FG_MINW 2
+#define FG_MINW 4
+#endif
+#ifndef FG_PACK_MINW
+#define FG_PACK_MINW 4
 #endif
 template <int B, int CLS, bool FULL, int MAXT, int NC>
-__global__ void __launch_bounds__(MAXT, (MAXT == 256 ? FG_MINW : 2)) k_encode(EncodeArgs a) {
+// i64 samples (32-bit input) and the tail kernels' LDS tables need the larger
+// register budget (2 waves/SIMD); the rest fits 128 VGPRs (4 waves/SIMD).
+__global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG_MINW : 2)) k_analyze(EncodeArgs a) {
     using ST = typename Cls<CLS>::S;
     using SumT = typename Cls<CLS>::Sum;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
     const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
     // the wave index is wave-uniform: keep it (and everything derived from it) in SGPRs
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l = lane_id();
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l0 = lane_id();
     const uint32_t C = NC ? (uint32_t)NC : a.channels;
     const uint32_t cw = 16u * C * B;           // dwords per 64-sample chunk
     const uint32_t cst = cw + stage_pad(C, B);  // LDS chunk stride (dwords)
-    const bool sep = FULL && a.stage_separate;
-    const LdsLayout LY = lds_layout(C, B, NW, a.image_bytes, FULL, sep);
-    uint32_t *stg = (uint32_t *)(smem + LY.stage);
-    uint32_t *img = (uint32_t *)(smem + LY.img);
+    const bool dbuf = FULL && a.stage_dbuf != 0;
+    const AnaLayout LY = ana_layout(C, B, NW, FULL, dbuf);
     uint8_t *par = smem + LY.par + wave * 512u;
     uint32_t *recs = (uint32_t *)(smem + LY.rec);
-    uint16_t *crct = (uint16_t *)(smem + LY.crc);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
-    for (uint32_t i = tid; i < 1024u; i += NT) crct[i] = a.crc_tab[i];
+    const bool stereo = a.stereo != 0;
+    const uint32_t cand = wave;
+    const uint32_t bd = a.bits + ((stereo && cand == 3) ? 1u : 0u);
 #ifdef FG_STAMPS
     uint64_t ph_[16] = {};
     uint64_t tprev_ = __builtin_amdgcn_s_memtime();
 #endif
 
-    // Persistent loop: this workgroup encodes frames blockIdx.x, +gridDim.x, ...; with a
-    // separate staging area the next frame's PCM is DMA'd in while this one is packed.
-    uint32_t jidx = blockIdx.x;
-    if (sep && jidx < a.n_jobs) stage_dma(a.pcm, a.jobs[jidx].pcm_off, stg, cw, cst, wave, NW, l);
-    for (; jidx < a.n_jobs; jidx += gridDim.x) {
+    // Persistent loop: this workgroup analyses frames blockIdx.x, +gridDim.x, ...; with double
+    // buffering the next frame's PCM is DMA'd into the idle staging buffer meanwhile.
+    uint32_t jidx = blockIdx.x, buf = 0;
+    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, a.jobs[jidx].pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0);
+    for (; jidx < a.n_jobs; jidx += gridDim.x, buf ^= 1u) {
+        const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
         const FrameJob job = a.jobs[jidx];
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
+        uint32_t *stg = (uint32_t *)(smem + (buf ? LY.stage1 : LY.stage0));
 
         // ---- 1. the frame's interleaved PCM in LDS (64 padded chunks of 64 samples)
-        if (sep) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            const uint32_t in_bytes = n * C * B;
-            const uint32_t *src = (const uint32_t *)(a.pcm + job.pcm_off);
-            const uint32_t nchunks = FULL ? 64u : (n + 63u) >> 6;
-            for (uint32_t ch = wave; ch < nchunks; ch += NW) {
-                for (uint32_t x = l; x < cw; x += 64) {
-                    const uint32_t wd = ch * cw + x;
-                    uint32_t v = 0;
-                    if (FULL || 4u * wd + 4u <= in_bytes) {
-                        v = src[wd];
-                    } else if (4u * wd < in_bytes) {
-                        const uint8_t *sb = (const uint8_t *)src + 4u * wd;
-                        for (uint32_t q = 0; 4u * wd + q < in_bytes; q++) v |= (uint32_t)sb[q] << (8 * q);
-                    }
-                    stg[ch * cst + x] = v;
-                }
-            }
-        }
+        if (dbuf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
         __syncthreads();
+        if (dbuf && jidx + gridDim.x < a.n_jobs)
+            stage_dma(a.pcm, a.jobs[jidx + gridDim.x].pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)),
+                      cw, cst, wave, NW, l);
         STAMP(0);
 
         // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
-        const bool stereo = a.stereo != 0;
-        const uint32_t cand = wave;
-        const uint32_t bd = a.bits + ((stereo && cand == 3) ? 1u : 0u);
         ST s[64];
-        {
-            // The candidate switch is hoisted out of the sample loops so each loop is
-            // branch-free and all 64 (or 128) LDS reads issue back to back.
-            const uint32_t *lw = stg + l * cst;
-            const uint32_t kind = stereo ? cand : 0u;  // 0 plain channel, 1 R, 2 mid, 3 side
-            const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand;
-            auto fill = [&](auto getL, auto getR) {
-                if (kind <= 1) {
-#pragma unroll
-                    for (int j = 0; j < 64; j++) {
-                        int64_t x = kind == 0 && !stereo ? getL(j, chan) : getL(j, chan);
-                        if (!FULL && l * 64u + j >= n) x = 0;
-                        s[j] = (ST)x;
-                    }
-                } else if (kind == 2) {  // mid from un-shifted L/R (encoder.zig:337,347)
-#pragma unroll
-                    for (int j = 0; j < 64; j++) {
-                        int64_t x = (getL(j, 0u) + getR(j)) >> 1;
-                        if (!FULL && l * 64u + j >= n) x = 0;
-                        s[j] = (ST)x;
-                    }
-                } else {  // side; 33-bit at 32 bps (samples64, encoder.zig:338)
-#pragma unroll
-                    for (int j = 0; j < 64; j++) {
-                        int64_t x = getL(j, 0u) - getR(j);
-                        if (!FULL && l * 64u + j >= n) x = 0;
-                        s[j] = (ST)x;
-                    }
-                }
-            };
-            if constexpr (NC == 2 && B == 4) {
-                // (L,R) dword pair per sample (8-B pad: conflict-free ds_read_b64)
-                const uint2 *p2 = (const uint2 *)lw;
-                fill([&](int j, uint32_t c) -> int64_t { return (int32_t)(c ? p2[j].y : p2[j].x); },
-                     [&](int j) -> int64_t { return (int32_t)p2[j].y; });
-            } else if constexpr (NC == 2 && B == 2 && !FG_NARROW) {
-                // (L,R) packed in one dword per sample (16-B pad: conflict-free ds_read_b128)
-                const uint32_t *p1 = lw;
-                fill([&](int j, uint32_t c) -> int64_t { return c ? ((int32_t)p1[j] >> 16) : ((int32_t)(p1[j] << 16) >> 16); },
-                     [&](int j) -> int64_t { return (int32_t)p1[j] >> 16; });
-            } else {
-                const uint8_t *base = (const uint8_t *)lw;
-                const uint32_t CB = C * B;
-                fill([&](int j, uint32_t c) -> int64_t { return ld_sample<B>(base + j * CB + c * B); },
-                     [&](int j) -> int64_t { return ld_sample<B>(base + j * CB + B); });
-            }
-        }
-        __syncthreads();  // staging is free from here on
-        if (sep && jidx + gridDim.x < a.n_jobs)
-            stage_dma(a.pcm, a.jobs[jidx + gridDim.x].pcm_off, stg, cw, cst, wave, NW, l);
+        load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, s);
         STAMP(1);
 
         // ---- 3. wasted bits (encoder.zig:556-570)
@@ -754,14 +723,10 @@ __global__ void __launch_bounds__(MAXT, (MAXT == 256 ? FG_MINW : 2)) k_encode(En
             if (CLS == 32 && T[k] == ~0ull) try_fixed = false;  // null -> VERBATIM (encoder.zig:520)
         }
         STAMP(3);
-#ifdef FG_CUT3
-        if (l == 0) a.frame_bytes[job.slot + cand] = k + R.type + (uint32_t)s[7] + (uint32_t)s[63];
-        continue;
-#endif
 
+        uint32_t seg = 0;  // exact bits of this lane's segment of the candidate subframe
         if (try_fixed) {
-            // ---- 6. residuals in place, s[j] := e_k (lane 0 keeps its k warm-up samples),
-            // and the finest-level partition sums (rice.zig:288-340)
+            // ---- 6. residuals in place and the finest-level partition sums (rice.zig:288-340)
             SumT S8[4] = {0, 0, 0, 0};
             uint32_t O8[4] = {0, 0, 0, 0};
             uint64_t *psum = nullptr;
@@ -785,38 +750,22 @@ __global__ void __launch_bounds__(MAXT, (MAXT == 256 ? FG_MINW : 2)) k_encode(En
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
             {
-                ST q1 = h1, q2 = h2, q3 = h3, q4 = h4;
-                auto body = [&](auto KK) {
-                    constexpr int K = decltype(KK)::value;
-#pragma unroll
-                    for (int j = 0; j < 64; j++) {
-                        const ST x = s[j];
-                        const ST r = fixed_residual<K, ST>(x, q1, q2, q3, q4);
-                        q4 = q3; q3 = q2; q2 = q1; q1 = x;
-                        const bool warm = (j < K) && (l == 0);
-                        if (!warm) s[j] = r;
-                        const uint32_t zz = zigzag32((int32_t)r);
-                        const uint32_t av = (zz >> 1) + (zz & 1u);  // |r|
-                        if constexpr (FULL) {
-                            S8[j >> 4] += warm ? 0u : av;
-                            O8[j >> 4] |= warm ? 0u : zz;
-                        } else {
-                            const uint32_t i = l * 64u + j;
-                            if (!warm && i < n) {
-                                const uint32_t pid = i / ps;
-                                atomicAdd((unsigned long long *)&psum[pid], (unsigned long long)av);
-                                atomicOr(&pmax[pid], zz);
-                            }
+                auto acc = [&](int j, bool warm, ST r) {
+                    const uint32_t zz = zigzag32((int32_t)r);
+                    const uint32_t av = (zz >> 1) + (zz & 1u);  // |r|
+                    if constexpr (FULL) {
+                        S8[j >> 4] += warm ? 0u : av;
+                        O8[j >> 4] |= warm ? 0u : zz;
+                    } else {
+                        const uint32_t i = l * 64u + j;
+                        if (!warm && i < n) {
+                            const uint32_t pid = i / ps;
+                            atomicAdd((unsigned long long *)&psum[pid], (unsigned long long)av);
+                            atomicOr(&pmax[pid], zz);
                         }
                     }
                 };
-                switch (k) {
-                    case 0: body(std::integral_constant<int, 0>()); break;
-                    case 1: body(std::integral_constant<int, 1>()); break;
-                    case 2: body(std::integral_constant<int, 2>()); break;
-                    case 3: body(std::integral_constant<int, 3>()); break;
-                    default: body(std::integral_constant<int, 4>()); break;
-                }
+                residuals_generic<ST>(s, h1, h2, h3, h4, l, k, acc);
             }
             STAMP(4);
 
@@ -951,36 +900,69 @@ __global__ void __launch_bounds__(MAXT, (MAXT == 256 ? FG_MINW : 2)) k_encode(En
                 R.order = k;
                 R.porder = best_o;
                 R.method = best_m;
-            } else {
-                // verbatim needs the samples back: invert the residual recurrence
-                ST q1 = h1, q2 = h2, q3 = h3, q4 = h4;
+                // ---- 9a. exact bits of the lane's segment (frame_writer.zig:299-372).  The
+                // residuals were not kept through the search (register pressure): reload the
+                // samples from the staged PCM and recompute them.
+                const uint32_t o = best_o, param_len = 4u + best_m, w = R.waste;
+                const uint8_t *pp = par + ((1u << o) - 1u);
+                if (l == 0) {
+                    const uint32_t p0 = pp[0];
+                    seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
+                }
+                load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, s);
+                if (w != 0) {
 #pragma unroll
-                for (int j = 0; j < 64; j++) {
-                    const bool warm = (l == 0 && (uint32_t)j < k);
-                    const ST x = warm ? s[j] : fixed_restore(k, s[j], q1, q2, q3, q4);
-                    s[j] = x;
-                    q4 = q3; q3 = q2; q2 = q1; q1 = x;
+                    for (int j = 0; j < 64; j++) s[j] >>= w;
+                }
+                const ST g1 = shr1(s[63]), g2 = shr1(s[62]), g3 = shr1(s[61]), g4 = shr1(s[60]);
+                if constexpr (FULL) {
+                    const uint32_t sh = 12u - o, psz = 4096u >> o;
+                    uint32_t pq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) pq[q] = pp[(l * 64u + 16u * q) >> sh];
+                    auto len_a = [&](int j, bool warm, ST r) {
+                        const uint32_t p = pq[j >> 4];
+                        const bool esc = (p & 0x80u) != 0;
+                        const uint32_t i = l * 64u + j;
+                        if ((j & 15) == 0 && i != 0 && (i & (psz - 1u)) == 0) seg += param_len + (esc ? 5u : 0u);
+                        const uint32_t zz = zigzag32((int32_t)r);
+                        const uint32_t cl = esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
+                        seg += warm ? 0u : cl;
+                    };
+                    residuals_generic<ST>(s, g1, g2, g3, g4, l, k, len_a);
+                } else {
+                    const uint32_t psz = n >> o;
+                    auto len_a = [&](int j, bool warm, ST r) {
+                        const uint32_t i = l * 64u + j;
+                        if (i < n && !warm) {
+                            const uint32_t p = pp[i / psz];
+                            const bool esc = (p & 0x80u) != 0;
+                            if (i != 0 && (i % psz) == 0) seg += param_len + (esc ? 5u : 0u);
+                            const uint32_t zz = zigzag32((int32_t)r);
+                            seg += esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
+                        }
+                    };
+                    residuals_generic<ST>(s, g1, g2, g3, g4, l, k, len_a);
                 }
             }
         }
+        if (R.type == 0) {
+            seg = (l == 0) ? 8u + bd : 0u;
+        } else if (R.type == 1) {
+            const uint32_t cnt = FULL ? 64u : (n > l * 64u ? min(64u, n - l * 64u) : 0u);
+            seg = cnt * bps + ((l == 0) ? 8u + R.waste : 0u);
+        }
+        const uint32_t sub_bits = wave_sum32(seg);
         STAMP(5);
-#ifdef FG_CUT5
-        if (l == 0) a.frame_bytes[job.slot + cand] = (uint32_t)R.est + R.type + R.porder + R.method + (uint32_t)s[5];
-        continue;
-#endif
 
-        // ---- 9. publish the candidate record, zero the frame image
+        // ---- 10. publish the candidate record; stereo decision (encoder.zig:441-452)
+        // or independent channels (:456-475)
         if (l == 0) {
             uint32_t *rc = recs + cand * 16u;
-            rc[0] = R.type; rc[1] = R.waste; rc[2] = R.bd; rc[3] = R.order; rc[4] = R.porder; rc[5] = R.method;
             rc[6] = (uint32_t)R.est; rc[7] = (uint32_t)(R.est >> 32);
+            rc[8] = sub_bits;
         }
         __syncthreads();
-        for (uint32_t i = tid; i < (a.image_bytes >> 4); i += NT) ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
-        __syncthreads();
-        STAMP(6);
-
-        // ---- 10. stereo decision (encoder.zig:441-452) or independent channels (:456-475)
         uint32_t channel_code, n_out;
         int my_slot;
         if (stereo) {
@@ -998,210 +980,59 @@ __global__ void __launch_bounds__(MAXT, (MAXT == 256 ? FG_MINW : 2)) k_encode(En
             const uint32_t c1 = (b == 0 || b == 2) ? 1u : 3u;
             my_slot = (cand == c0) ? 0 : ((cand == c1) ? 1 : -1);
             n_out = 2;
+            misc[8] = c0;
+            misc[9] = c1;
         } else {
             channel_code = C - 1u;
             n_out = C;
             my_slot = (int)cand;
         }
-        if (tid == 0) misc[16] = 8u * write_frame_header(img, job.number, a.bits, channel_code, n, a.sample_rate);
 
-        // ---- 11. exact subframe lengths (pass A), frame_writer.zig:269-372
-        uint32_t lane_off = 0;
-        uint32_t pq[4] = {0, 0, 0, 0};
-        const uint32_t param_len = 4u + R.method;
-        const uint32_t w = R.waste;
-        k = R.order;
+        // ---- 11. the frame descriptor
+        uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
         const uint8_t *pp = par + ((1u << R.porder) - 1u);
         if (my_slot >= 0) {
-            uint32_t seg = 0;
-            if (R.type == 0) {
-                seg = (l == 0) ? 8u + bd : 0u;
-            } else if (R.type == 1) {
-                const uint32_t cnt = FULL ? 64u : (n > l * 64u ? min(64u, n - l * 64u) : 0u);
-                seg = cnt * bps + ((l == 0) ? 8u + w : 0u);
-            } else {
-                const uint32_t o = R.porder;
-                if (l == 0) {
-                    const uint32_t p0 = pp[0];
-                    seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
-                }
-                if constexpr (FULL) {
-                    const uint32_t sh = 12u - o, psz = 4096u >> o;
-#pragma unroll
-                    for (int q = 0; q < 4; q++) pq[q] = pp[(l * 64u + 16u * q) >> sh];
-#pragma unroll
-                    for (int j = 0; j < 64; j++) {
-                        const uint32_t p = pq[j >> 4];
-                        const bool esc = (p & 0x80u) != 0;
-                        const uint32_t i = l * 64u + j;
-                        if ((j & 15) == 0 && i != 0 && (i & (psz - 1u)) == 0) seg += param_len + (esc ? 5u : 0u);
-                        const bool warm = (j < 4) && (l == 0 && (uint32_t)j < k);
-                        const uint32_t zz = zigzag32((int32_t)s[j]);
-                        const uint32_t cl = esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
-                        seg += warm ? 0u : cl;
-                    }
-                } else {
-                    const uint32_t psz = n >> o;
-#pragma unroll
-                    for (int j = 0; j < 64; j++) {
-                        const uint32_t i = l * 64u + j;
-                        if (i < n && !(l == 0 && (uint32_t)j < k)) {
-                            const uint32_t p = pp[i / psz];
-                            const bool esc = (p & 0x80u) != 0;
-                            if (i != 0 && (i % psz) == 0) seg += param_len + (esc ? 5u : 0u);
-                            const uint32_t zz = zigzag32((int32_t)s[j]);
-                            seg += esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
-                        }
-                    }
-                }
+            SubDesc *sd = (SubDesc *)(fd + sizeof(FrameDesc)) + my_slot;
+            if (l == 0) {
+                sd->type = (uint8_t)R.type;
+                sd->waste = (uint8_t)R.waste;
+                sd->bd = (uint8_t)R.bd;
+                sd->order = (uint8_t)R.order;
+                sd->porder = (uint8_t)R.porder;
+                sd->method = (uint8_t)R.method;
+                sd->cand = (uint8_t)cand;
+                sd->bits = sub_bits;
+                sd->cval = R.cval;
             }
-            const uint32_t incl = wave_incl_scan32(seg);
-            lane_off = incl - seg;
-            if (l == 63) misc[my_slot] = incl;
-        }
-        __syncthreads();
-        STAMP(7);
-
-        uint32_t total_bits = misc[16];
-        uint32_t sub_start = total_bits;
-        for (uint32_t i = 0; i < n_out; i++) {
-            if ((int)i < my_slot) sub_start += misc[i];
-            total_bits += misc[i];
-        }
-        STAMP(8);
-
-        // ---- 12. pack (pass B): each lane writes its contiguous bit segment
-        if (my_slot >= 0) {
-#if FG_WRITER_ATOMIC
-            AtomicWriter bw;
-#else
-            LaneWriter bw;
-#endif
-            bw.init(img, sub_start + lane_off);
-            if (R.type == 0) {
-                if (l == 0) {  // writeConstantSubframe: header 0x00, value << waste in bd bits, no wasted flag
-                    bw.put(0, 8);
-                    bw.put(((uint64_t)R.cval << w) & (~0ull >> (64 - bd)), bd);
-                }
-            } else {
-                const uint64_t mask = ~0ull >> (64 - bps);
-                if (l == 0) {
-                    const uint32_t hdr = (R.type == 1) ? (w ? 0x03u : 0x02u) : (((8u | k) << 1) | (w ? 1u : 0u));
-                    bw.put(hdr, 8);
-                    if (w) bw.put(1, w);
-                }
-                if (R.type == 1) {
-#pragma unroll
-                    for (int j = 0; j < 64; j++)
-                        if (FULL || l * 64u + j < n) bw.put((uint64_t)(int64_t)s[j] & mask, bps);
-                } else {
-                    const uint32_t o = R.porder;
-                    auto part_header = [&](uint32_t p) {
-                        if (p & 0x80u) {
-                            bw.put(0x0Fu | (R.method << 4), param_len);
-                            bw.put(p & 0x7Fu, 5);
-                        } else {
-                            bw.put(p, param_len);
-                        }
-                    };
-                    if (l == 0) {
-#pragma unroll
-                        for (int j = 0; j < 4; j++)  // warm-up samples
-                            if ((uint32_t)j < k) bw.put((uint64_t)(int64_t)s[j] & mask, bps);
-                        bw.put((R.method << 4) | o, 6);
-                        part_header(pp[0]);
-                    }
-                    auto code = [&](int32_t r, uint32_t p) {
-                        if (p & 0x80u) {
-                            const uint32_t len = p & 0x7Fu;
-                            if (len) bw.put((uint64_t)(uint32_t)r & (~0ull >> (64 - len)), len);
-                        } else {
-                            const uint32_t zz = zigzag32(r);
-                            bw.zeros(zz >> p);
-                            bw.put((1u << p) | (zz & ((1u << p) - 1u)), p + 1u);
-                        }
-                    };
-                    if constexpr (FULL) {
-                        const uint32_t psz = 4096u >> o;
-#pragma unroll
-                        for (int j = 0; j < 64; j++) {
-                            const uint32_t i = l * 64u + j;
-                            if ((j & 15) == 0 && i != 0 && (i & (psz - 1u)) == 0) part_header(pq[j >> 4]);
-                            if (!((j < 4) && l == 0 && (uint32_t)j < k)) code((int32_t)s[j], pq[j >> 4]);
-                        }
-                    } else {
-                        const uint32_t psz = n >> o;
-#pragma unroll
-                        for (int j = 0; j < 64; j++) {
-                            const uint32_t i = l * 64u + j;
-                            if (i < n && !(l == 0 && (uint32_t)j < k)) {
-                                const uint32_t p = pp[i / psz];
-                                if (i != 0 && (i % psz) == 0) part_header(p);
-                                code((int32_t)s[j], p);
-                            }
-                        }
-                    }
-                }
+            sd->lane_bits[l] = seg;
+            if (R.type == 2) {
+                const uint32_t np = 1u << R.porder;
+                for (uint32_t j = l; j < np; j += 64) sd->params[j] = pp[j];
             }
-            bw.finish();
         }
-        STAMP(9);
-        __syncthreads();
-        STAMP(10);
-
-        // ---- 13. CRC-16 of the frame (frame_writer.zig:111-125,144-148): the word stream is
-        // front-padded with zero words (a no-op for an init-0 CRC) to NT*SW words; thread t folds
-        // its SW words as two interleaved halves, joins them (x z^(32*SW/2)), shifts the result by
-        // z^(32*SW*(NT-1-t)) and the workgroup XOR-reduces.
-        const uint32_t Lb = (total_bits + 7u) >> 3;
-        const uint32_t W4 = Lb >> 2;
-        {
-            const uint32_t SW = a.crc_seg_words, H = SW >> 1;
-            const int32_t Z = (int32_t)(NT * SW) - (int32_t)W4;
-            uint32_t ca = 0, cb = 0;
-            const int32_t va = (int32_t)(tid * SW) - Z, vb = va + (int32_t)H;
-            for (uint32_t i = 0; i < H; i++) {
-                const int32_t ra = va + (int32_t)i, rb = vb + (int32_t)i;
-                if (ra >= 0) ca = crc_word(ca, img[ra], crct);
-                if (rb >= 0) cb = crc_word(cb, img[rb], crct);
-            }
-            const uint32_t ct = (ca ? crc_mulmod(ca, a.crc_pow[NT]) : 0u) ^ cb;
-            uint32_t contrib = ct ? crc_mulmod(ct, a.crc_pow[tid]) : 0u;
-            contrib = wave_xor32(contrib);
-            if (l == 0) misc[24 + wave] = contrib;
-        }
-        __syncthreads();
         if (tid == 0) {
-            uint32_t crc = 0;
-            for (uint32_t i = 0; i < NW; i++) crc ^= misc[24 + i];
-            for (uint32_t b = W4 * 4u; b < Lb; b++)
-                crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
-            put_bits(img, Lb * 8u, crc, 16);
-            const uint32_t fbytes = Lb + 2u;
-            if (fbytes + 16u > a.slot_bytes || fbytes > a.image_bytes) atomicOr(a.err, 1u);
+            uint32_t *hw = misc + 32;
+            hw[0] = hw[1] = hw[2] = hw[3] = 0;
+            const uint32_t hb = write_frame_header(hw, job.number, a.bits, channel_code, n, a.sample_rate);
+            uint32_t total = 8u * hb;
+            if (stereo) total += recs[misc[8] * 16 + 8] + recs[misc[9] * 16 + 8];
+            else
+                for (uint32_t c = 0; c < C; c++) total += recs[c * 16 + 8];
+            FrameDesc *f = (FrameDesc *)fd;
+            f->hdr_bytes = hb;
+            f->total_bits = total;
+            f->channel_code = channel_code;
+            f->n_out = n_out;
+            f->hdr[0] = hw[0]; f->hdr[1] = hw[1]; f->hdr[2] = hw[2]; f->hdr[3] = hw[3];
+            const uint32_t fbytes = ((total + 7u) >> 3) + 2u;
+            if (fbytes + 16u > a.image_bytes) atomicOr(a.err, 1u);  // the pack kernel's image bound
             a.frame_bytes[job.slot] = fbytes;
             misc[17] = fbytes;
         }
-        __syncthreads();
-        STAMP(11);
 
-        // ---- 14. frame image -> its slot (big-endian words to bytes)
-        {
-            const uint32_t fbytes = misc[17];
-            const uint32_t units = min((fbytes + 15u) >> 4, a.slot_bytes >> 4);
-            uint4 *dst = (uint4 *)(a.slots + (uint64_t)job.slot * a.slot_bytes);
-            for (uint32_t u = tid; u < units; u += NT) {
-                uint4 v = ((const uint4 *)img)[u];
-                v.x = __builtin_bswap32(v.x);
-                v.y = __builtin_bswap32(v.y);
-                v.z = __builtin_bswap32(v.z);
-                v.w = __builtin_bswap32(v.w);
-                dst[u] = v;
-            }
-        }
-
-        // ---- 15. optional decision records (parity tests)
+        // ---- 12. optional decision records (parity tests)
         if (a.records) {
+            __syncthreads();
             FrameRec *fr = a.records + job.slot;
             SubRec *sr = &fr->cand[cand];
             if (l == 0) {
@@ -1226,28 +1057,252 @@ __global__ void __launch_bounds__(MAXT, (MAXT == 256 ? FG_MINW : 2)) k_encode(En
                 fr->pad = 0;
             }
         }
-        __syncthreads();  // image / params / scratch are reused by the next frame
-        STAMP(12);
+        __syncthreads();  // params / records / scratch are reused by the next frame
+        STAMP(6);
     }  // persistent frame loop
 #ifdef FG_STAMPS
     if (l == 0 && a.stamps)
-        for (int i = 0; i < 13; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
+        for (int i = 0; i < 7; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
 #endif
 }
 
-// persistent launch: grid = min(frames, resident workgroups)
+// ------------------------------------------------------------------------
+// Kernel 3: frame packing.  One workgroup per frame (persistent loop), one
+// wave per written subframe.  Recomputes the chosen subframe's samples and
+// residuals from the PCM (cheaper than storing them), packs the frame into an
+// LDS image with every lane writing its own bit segment at the offset the
+// analysis kernel measured (frame_writer.zig:269-372), appends the CRC-16
+// (frame_writer.zig:111-125,144-148) and stores the frame at its final byte
+// offset in the output bitstream.
+// ------------------------------------------------------------------------
 template <int B, int CLS, bool FULL, int MAXT, int NC>
-static hipError_t launch_encode_t(const EncodeArgs &a, uint32_t threads, uint32_t lds, hipStream_t st) {
-    auto k = k_encode<B, CLS, FULL, MAXT, NC>;
+__global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL) ? FG_PACK_MINW : 2)) k_pack(EncodeArgs a) {
+    using ST = typename Cls<CLS>::S;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+    const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l0 = lane_id();
+    const uint32_t C = NC ? (uint32_t)NC : a.channels;
+    const uint32_t cw = 16u * C * B;
+    const uint32_t cst = cw + stage_pad(C, B);
+    const PackLayout LY = pack_layout(C, B, a.image_bytes);
+    uint32_t *stg = (uint32_t *)(smem + LY.stage);
+    uint32_t *img = (uint32_t *)(smem + LY.img);
+    uint16_t *crct = (uint16_t *)(smem + LY.crc);
+    uint32_t *misc = (uint32_t *)(smem + LY.misc);
+    for (uint32_t i = tid; i < 1024u; i += NT) crct[i] = a.crc_tab[i];
+    const bool stereo = a.stereo != 0;
+
+    for (uint32_t jidx = blockIdx.x; jidx < a.n_jobs; jidx += gridDim.x) {
+        const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
+        const FrameJob job = a.jobs[jidx];
+        const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
+        const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
+        const FrameDesc *F = (const FrameDesc *)fd;
+        const SubDesc *sd = (const SubDesc *)(fd + sizeof(FrameDesc)) + wave;
+        const uint32_t total_bits = F->total_bits;
+        const uint32_t fbytes = ((total_bits + 7u) >> 3) + 2u;
+        const uint64_t D = a.offsets[job.slot];
+        if (fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap) {  // uniform: skip the frame
+            if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
+            continue;
+        }
+        const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
+                       method = sd->method, cand = sd->cand;
+
+        // ---- 1. PCM -> LDS, candidate samples -> VGPRs
+        stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
+        __syncthreads();
+        ST s[64];
+        load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, s);  // (unused for CONSTANT)
+        // lane offsets from the measured segment lengths (uniform prefix of earlier subframes)
+        const uint32_t seg = sd->lane_bits[l];
+        uint32_t sub_start = 8u * F->hdr_bytes;
+        for (uint32_t t = 0; t < wave; t++) sub_start += ((const SubDesc *)(fd + sizeof(FrameDesc)) + t)->bits;
+        const uint32_t lane_off = wave_incl_scan32(seg) - seg;
+        __syncthreads();  // staging dead: zero the image
+        const uint32_t Wz = (fbytes + 3u) / 4u + 2u;
+        for (uint32_t i = tid; i < Wz; i += NT) img[i] = 0;
+        __syncthreads();
+        if (tid < 4) {
+            const uint32_t hv = F->hdr[tid];
+            if (hv) atomicOr(&img[tid], hv);
+        }
+
+        // ---- 2. waste shift and residuals (fixed.zig:30-81)
+        const uint32_t bps = bd - w;
+        if (type != 0 && w != 0) {
+#pragma unroll
+            for (int j = 0; j < 64; j++) s[j] >>= w;
+        }
+        if (type == 2) {
+            const ST h1 = shr1(s[63]), h2 = shr1(s[62]), h3 = shr1(s[61]), h4 = shr1(s[60]);
+            auto none = [](int, bool, ST) {};
+            residuals_generic<ST>(s, h1, h2, h3, h4, l, k, none);
+        }
+
+        // ---- 3. pack: each lane writes its contiguous bit segment (frame_writer.zig:269-372).
+        // Every field is ORed into the zeroed image at its bit position; the per-sample
+        // code is branch-free (escape/rice/warm-up/partition header selected per lane).
+        {
+            uint32_t pos = sub_start + lane_off;
+            const uint64_t mask = ~0ull >> (64 - (bps ? bps : 1u));
+            if (l == 0) {
+                AtomicWriter bw;
+                bw.init(img, pos);
+                if (type == 0) {  // writeConstantSubframe: header 0x00, value << waste in bd bits, no wasted flag
+                    bw.put(0, 8);
+                    bw.put(((uint64_t)sd->cval << w) & (~0ull >> (64 - bd)), bd);
+                } else {
+                    const uint32_t hdr = (type == 1) ? (w ? 0x03u : 0x02u) : (((8u | k) << 1) | (w ? 1u : 0u));
+                    bw.put(hdr, 8);
+                    if (w) bw.put(1, w);
+                    if (type == 2) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++)  // warm-up samples
+                            if ((uint32_t)j < k) bw.put((uint64_t)(int64_t)s[j] & mask, bps);
+                        bw.put((method << 4) | o, 6);
+                        const uint32_t p0 = sd->params[0];
+                        if (p0 & 0x80u) {
+                            bw.put(0x0Fu | (method << 4), 4u + method);
+                            bw.put(p0 & 0x7Fu, 5);
+                        } else {
+                            bw.put(p0, 4u + method);
+                        }
+                    }
+                }
+                pos = bw.pos;
+            }
+            if (type == 1) {
+#pragma unroll
+                for (int j = 0; j < 64; j++) {
+                    const bool ok = FULL || l * 64u + j < n;
+                    put_or2(img, pos, (uint64_t)(int64_t)s[j] & mask, ok ? bps : 0u);
+                    pos += ok ? bps : 0u;
+                }
+            } else if (type == 2) {
+                const uint32_t param_len = 4u + method;
+                const uint32_t esc_code = (0x0Fu | (method << 4)) << 5;
+                const uint8_t *pp = sd->params;
+                // one residual: rice (q zeros, 1, p low bits) or escape (raw w-bit two's complement)
+                auto code = [&](int32_t r, uint32_t p, bool skip) {
+                    const bool esc = (p & 0x80u) != 0;
+                    const uint32_t wb = p & 0x7Fu;
+                    const uint32_t zz = zigzag32(r);
+                    const uint32_t pr = esc ? 0u : p;
+                    const uint32_t qz = (esc || skip) ? 0u : (zz >> pr);
+                    const uint64_t v = esc ? ((uint64_t)(uint32_t)r & (~0ull >> (64 - (wb ? wb : 1u))))
+                                           : (uint64_t)((1u << pr) | (zz & ((1u << pr) - 1u)));
+                    const uint32_t len = skip ? 0u : (esc ? wb : pr + 1u);
+                    pos += qz;
+                    put_or2(img, pos, v, len);
+                    pos += len;
+                };
+                auto part_header = [&](uint32_t p, bool on) {
+                    const bool esc = (p & 0x80u) != 0;
+                    const uint32_t hl = on ? param_len + (esc ? 5u : 0u) : 0u;
+                    put_or2(img, pos, esc ? (esc_code | (p & 0x7Fu)) : p, hl);
+                    pos += hl;
+                };
+                if constexpr (FULL) {
+                    const uint32_t sh = 12u - o, psz = 4096u >> o;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t p = pp[(l * 64u + 16u * q) >> sh];
+                        const uint32_t i0 = l * 64u + 16u * q;
+                        part_header(p, i0 != 0 && (i0 & (psz - 1u)) == 0);
+#pragma unroll
+                        for (int jj = 0; jj < 16; jj++) {
+                            const int j = 16 * q + jj;
+                            code((int32_t)s[j], p, j < 4 && l == 0 && (uint32_t)j < k);
+                        }
+                    }
+                } else {
+                    const uint32_t psz = n >> o;
+#pragma unroll
+                    for (int j = 0; j < 64; j++) {
+                        const uint32_t i = l * 64u + j;
+                        const bool ok = i < n;
+                        const uint32_t p = ok ? pp[i / psz] : 0u;
+                        part_header(p, ok && i != 0 && (i % psz) == 0);
+                        code((int32_t)s[j], p, !ok || (l == 0 && (uint32_t)j < k));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- 4. CRC-16 of the frame: the word stream is front-padded with zero words (a no-op
+        // for an init-0 CRC) to NT*2H words; thread t folds its 2H words as two interleaved
+        // halves, joins them (x z^(32H)), shifts by z^(64H(NT-1-t)) and the workgroup
+        // XOR-reduces.  H is odd so the per-thread word stride 2H costs at most 2-way conflicts.
+        const uint32_t Lb = (total_bits + 7u) >> 3;
+        const uint32_t W4 = Lb >> 2;
+        {
+            uint32_t H = (W4 + 2u * NT - 1u) / (2u * NT);
+            H = H | 1u;
+            const int32_t Z = (int32_t)(NT * 2u * H) - (int32_t)W4;
+            uint32_t ca = 0, cb = 0;
+            const int32_t va = (int32_t)(tid * 2u * H) - Z, vb = va + (int32_t)H;
+            for (uint32_t i = 0; i < H; i++) {
+                const int32_t ra = va + (int32_t)i, rb = vb + (int32_t)i;
+                if (ra >= 0) ca = crc_word(ca, img[ra], crct);
+                if (rb >= 0) cb = crc_word(cb, img[rb], crct);
+            }
+            const uint32_t ct = (ca ? crc_mulmod(ca, a.crc_join[H - 1u]) : 0u) ^ cb;
+            uint32_t contrib = ct ? crc_mulmod(ct, a.crc_pow[(H - 1u) * NT + tid]) : 0u;
+            contrib = wave_xor32(contrib);
+            if (l == 0) misc[wave] = contrib;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t crc = 0;
+            for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
+            for (uint32_t b = W4 * 4u; b < Lb; b++)
+                crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+            put_bits(img, Lb * 8u, crc, 16);
+        }
+        __syncthreads();
+
+        // ---- 5. image -> out[D, D + fbytes): big-endian words realigned to the byte offset
+        {
+            const uint64_t E = D + fbytes;
+            const uint64_t q0 = D >> 2, q1 = (E + 3u) >> 2;
+            const uint32_t sa = (uint32_t)(D & 3u);
+            uint32_t *o32 = (uint32_t *)a.out;
+            for (uint64_t q = q0 + tid; q < q1; q += NT) {
+                const uint32_t m = (uint32_t)(q - q0);
+                const uint32_t lo = img[m];
+                const uint32_t hi = m ? img[m - 1u] : 0u;
+                const uint32_t v = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(hi, lo, sa) : lo);
+                const uint64_t b0 = 4u * q;
+                if (b0 >= D && b0 + 4u <= E) {
+                    o32[q] = v;
+                } else {
+#pragma unroll
+                    for (uint32_t b = 0; b < 4; b++)
+                        if (b0 + b >= D && b0 + b < E) a.out[b0 + b] = (uint8_t)(v >> (8 * b));
+                }
+            }
+        }
+        __syncthreads();  // the image / staging area is reused by the next frame
+    }  // persistent frame loop
+}
+
+// persistent launch: grid = min(frames, resident workgroups)
+template <typename KernelT>
+static hipError_t launch_persistent(KernelT k, const EncodeArgs &a, uint32_t threads, uint32_t lds, hipStream_t st) {
     struct Occ {
+        const void *fn;
         uint32_t threads, lds;
         int resident;
     };
-    static Occ cache[8];
+    static Occ cache[16];
     static int n_cache = 0, cus = 0;
     int resident = 0;
     for (int i = 0; i < n_cache; i++)
-        if (cache[i].threads == threads && cache[i].lds == lds) resident = cache[i].resident;
+        if (cache[i].fn == (const void *)k && cache[i].threads == threads && cache[i].lds == lds)
+            resident = cache[i].resident;
     if (!resident) {
         hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
@@ -1257,7 +1312,7 @@ static hipError_t launch_encode_t(const EncodeArgs &a, uint32_t threads, uint32_
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k, (int)threads, (size_t)lds);
         if (e != hipSuccess) return e;
         resident = nb > 0 ? nb : 1;
-        if (n_cache < 8) cache[n_cache++] = {threads, lds, resident};
+        if (n_cache < 16) cache[n_cache++] = {(const void *)k, threads, lds, resident};
     }
     uint64_t grid = a.n_jobs;
     const uint64_t cap = (uint64_t)resident * (uint64_t)(cus > 0 ? cus : 256);
@@ -1267,15 +1322,22 @@ static hipError_t launch_encode_t(const EncodeArgs &a, uint32_t threads, uint32_
     return hipGetLastError();
 }
 
-// NC = 2 for two channels, 1 for mono, 0 (runtime) otherwise; MAXT by wave count
+// NC = 2 for two channels, 1 for mono, 0 (runtime) otherwise; MAXT by wave count.
+// stage: 0 = analysis, 1 = pack.
 template <int B, int CLS>
-static hipError_t launch_encode_b(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st) {
-#define FG_L(NCV, MT)                                                                  \
-    return full ? launch_encode_t<B, CLS, true, MT, NCV>(a, threads, lds, st)          \
-                : launch_encode_t<B, CLS, false, MT, NCV>(a, threads, lds, st)
-    if (a.channels == 2) { FG_L(2, 256); }
-    if (a.channels == 1) { FG_L(1, 256); }
-    if (threads <= 256) { FG_L(0, 256); }
+static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds,
+                                 hipStream_t st) {
+#define FG_L(NCV, MT)                                                                                     \
+    do {                                                                                                  \
+        if (stage == 0)                                                                                   \
+            return full ? launch_persistent(k_analyze<B, CLS, true, MT, NCV>, a, threads, lds, st)       \
+                        : launch_persistent(k_analyze<B, CLS, false, MT, NCV>, a, threads, lds, st);     \
+        return full ? launch_persistent(k_pack<B, CLS, true, MT, NCV>, a, threads, lds, st)              \
+                    : launch_persistent(k_pack<B, CLS, false, MT, NCV>, a, threads, lds, st);            \
+    } while (0)
+    if (a.channels == 2) FG_L(2, 256);
+    if (a.channels == 1) FG_L(1, 256);
+    if (threads <= 256) FG_L(0, 256);
     FG_L(0, 512);
 #undef FG_L
 }

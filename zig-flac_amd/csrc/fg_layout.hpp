@@ -4,15 +4,24 @@
 
 namespace fg {
 
-struct LdsLayout {
-    uint32_t stage;  // PCM staging: 64 padded chunks
-    uint32_t img;    // frame image (big-endian 32-bit words)
-    uint32_t par;    // rice params, 512 B per candidate wave (orders 0..8 at offset (1<<o)-1)
-    uint32_t rec;    // 16 x u32 per candidate wave
-    uint32_t crc;    // 4 x 256 u16 CRC tables
-    uint32_t misc;   // 64 x u32 scratch (sub lengths, crc partials, header bits)
+// Analysis kernel (one wave per candidate, nw waves).
+struct AnaLayout {
+    uint32_t stage0; // PCM staging: 64 padded chunks
+    uint32_t stage1; // second staging buffer (double-buffered LDS-DMA prefetch), or == stage0
     uint32_t psum;   // tail kernel only: 2 x 256 u64 per wave
     uint32_t pmax;   // tail kernel only: 2 x 256 u32 per wave
+    uint32_t par;    // rice params, 512 B per candidate wave (orders 0..8 at offset (1<<o)-1)
+    uint32_t rec;    // 16 x u32 per candidate wave
+    uint32_t misc;   // 64 x u32 scratch (header words)
+    uint32_t total;
+};
+
+// Pack kernel (one wave per written subframe): staging, then the frame image.
+struct PackLayout {
+    uint32_t stage;  // PCM staging (aliases the image)
+    uint32_t img;    // frame image (big-endian 32-bit words)
+    uint32_t crc;    // 4 x 256 u16 CRC tables
+    uint32_t misc;   // 64 x u32 scratch (crc partials)
     uint32_t total;
 };
 
@@ -29,32 +38,38 @@ __host__ __device__ inline uint32_t stage_bytes(uint32_t C, uint32_t B) {
     return 64u * (16u * C * B + stage_pad(C, B)) * 4u;
 }
 
-// Full-frame kernel with `separate` staging: the staging area is its own region
-// so the next frame's PCM can land (LDS-DMA) while the current frame is packed.
-// Otherwise (tail kernel, or configs whose two regions exceed 160 KiB) one
-// region holds, in turn, the staging area, the per-wave partition tables (tail
-// kernel), then the frame image.
-__host__ __device__ inline LdsLayout lds_layout(uint32_t C, uint32_t B, uint32_t nw, uint32_t image_bytes, bool full,
-                                               bool separate) {
-    LdsLayout L;
-    uint32_t end;
-    if (full && separate) {
-        L.stage = 0;
-        L.img = fg_round16(stage_bytes(C, B));
-        L.psum = L.pmax = 0;
-        end = L.img + fg_round16(image_bytes);
-    } else {
-        uint32_t r0 = stage_bytes(C, B);
-        if (image_bytes > r0) r0 = image_bytes;
-        if (!full && nw * 6144u > r0) r0 = nw * 6144u;
-        L.stage = L.img = 0;
-        L.psum = 0;
-        L.pmax = nw * 4096u;
-        end = fg_round16(r0);
+// The staged PCM of a frame stays valid for the whole analysis (the chosen
+// candidate's residuals are recomputed from it for the exact-length pass).
+// The full-frame kernel double-buffers it when both buffers fit and DMAs the
+// next frame's PCM into the idle one; the tail kernel (and configs whose two
+// buffers do not fit) stage synchronously into one buffer.
+__host__ __device__ inline AnaLayout ana_layout(uint32_t C, uint32_t B, uint32_t nw, bool full, bool dbuf) {
+    AnaLayout L;
+    const uint32_t sb = fg_round16(stage_bytes(C, B));
+    uint32_t end = sb;
+    L.stage0 = L.stage1 = 0;
+    if (full && dbuf) {
+        L.stage1 = sb;
+        end = 2u * sb;
+    }
+    L.psum = L.pmax = end;
+    if (!full) {
+        L.pmax = end + nw * 4096u;
+        end += nw * 6144u;
     }
     L.par = end;
     L.rec = L.par + nw * 512u;
-    L.crc = L.rec + nw * 64u;
+    L.misc = L.rec + nw * 64u;
+    L.total = fg_round16(L.misc + 256u);
+    return L;
+}
+
+__host__ __device__ inline PackLayout pack_layout(uint32_t C, uint32_t B, uint32_t image_bytes) {
+    PackLayout L;
+    uint32_t r0 = stage_bytes(C, B);
+    if (image_bytes > r0) r0 = image_bytes;
+    L.stage = L.img = 0;
+    L.crc = fg_round16(r0);
     L.misc = L.crc + 2048u;
     L.total = fg_round16(L.misc + 256u);
     return L;

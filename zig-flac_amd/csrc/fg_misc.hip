@@ -1,6 +1,7 @@
 // fg_misc.hip -- the small kernels around the frame encoder (gfx950): frame
-// table, size scan, compaction into contiguous bitstreams, MD5 (md5.zig /
-// RFC 1321) with one lane per independent stream, and the encode dispatcher.
+// table, frame-size scan, MD5 (md5.zig / RFC 1321) with one lane per
+// independent stream, and the per-width dispatcher of the analysis / pack
+// kernels.
 #include <hip/hip_runtime.h>
 
 #include "fg_common.hpp"
@@ -9,17 +10,18 @@ namespace fg {
 
 __device__ __forceinline__ uint32_t lane_id_m() { return __lane_id(); }
 
-hipError_t launch_encode_b1(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
-hipError_t launch_encode_b2(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
-hipError_t launch_encode_b3(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
-hipError_t launch_encode_b4(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_stage_b1(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_stage_b2(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_stage_b3(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+hipError_t launch_stage_b4(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
 
-hipError_t launch_encode(const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st) {
+// stage 0: analysis kernel, 1: pack kernel
+hipError_t launch_stage(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st) {
     switch (a.bytes_per_sample) {
-        case 1: return launch_encode_b1(a, full, threads, lds, st);
-        case 2: return launch_encode_b2(a, full, threads, lds, st);
-        case 3: return launch_encode_b3(a, full, threads, lds, st);
-        case 4: return launch_encode_b4(a, full, threads, lds, st);
+        case 1: return launch_stage_b1(stage, a, full, threads, lds, st);
+        case 2: return launch_stage_b2(stage, a, full, threads, lds, st);
+        case 3: return launch_stage_b3(stage, a, full, threads, lds, st);
+        case 4: return launch_stage_b4(stage, a, full, threads, lds, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -71,47 +73,6 @@ __global__ void __launch_bounds__(1024) k_scan(const uint32_t *sizes, uint64_t *
         uint64_t tot = 0;
         for (int i = 0; i < 16; i++) tot += wsum[i];
         *total = tot;
-    }
-}
-
-// ------------------------------------------------------------------------
-// compaction: frame slots -> contiguous byte stream
-// ------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_compact(const uint8_t *slots, uint32_t slot_bytes, const uint32_t *sizes,
-                                                 const uint64_t *offsets, uint8_t *out, uint64_t out_cap, uint32_t *err) {
-    const uint32_t f = blockIdx.x;
-    const uint64_t D = offsets[f];
-    const uint32_t len = sizes[f];
-    if (D + len > out_cap) {
-        if (threadIdx.x == 0) atomicOr(err, 2u);
-        return;
-    }
-    const uint8_t *src = slots + (uint64_t)f * slot_bytes;
-    const uint64_t E = D + len;
-    const uint64_t w0 = (D + 3) >> 2, w1 = E >> 2;  // fully covered dwords [w0, w1)
-    uint32_t *o32 = (uint32_t *)out;
-    const uint32_t *s32 = (const uint32_t *)src;
-    if (w1 > w0) {
-        const uint32_t sh = (uint32_t)((4 * w0 - D) & 3);  // source byte offset of dword w0 is 4*w0 - D
-        const uint64_t sbase = 4 * w0 - D;
-        for (uint64_t w = w0 + threadIdx.x; w < w1; w += blockDim.x) {
-            const uint64_t sb = sbase + 4 * (w - w0);
-            const uint32_t lo = s32[sb >> 2];
-            uint32_t v = lo;
-            if (sh) {
-                const uint32_t hi = s32[(sb >> 2) + 1];
-                v = __builtin_amdgcn_alignbyte(hi, lo, sh);
-            }
-            o32[w] = v;
-        }
-        if (threadIdx.x < 8) {
-            // head bytes [D, 4*w0) and tail bytes [4*w1, E)
-            uint64_t b = threadIdx.x < 4 ? D + threadIdx.x : 4 * w1 + (threadIdx.x - 4);
-            bool ok = threadIdx.x < 4 ? (b < 4 * w0) : (b < E);
-            if (ok) out[b] = src[b - D];
-        }
-    } else {
-        for (uint64_t b = D + threadIdx.x; b < E; b += blockDim.x) out[b] = src[b - D];
     }
 }
 
@@ -245,13 +206,6 @@ hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, 
 
 hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, hipStream_t st) {
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, sizes, offsets, total, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_compact(const uint8_t *slots, uint32_t slot_bytes, const uint32_t *sizes, const uint64_t *offsets,
-                          uint8_t *out, uint64_t out_cap, uint32_t *err, uint32_t n, hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3(n), dim3(256), 0, st, slots, slot_bytes, sizes, offsets, out, out_cap, err);
     return hipGetLastError();
 }
 

@@ -27,8 +27,8 @@ ERRORS = {
     -6: "InternalError",
 }
 
-K_ENCODE, K_ENCODE_TAIL, K_SCAN, K_COMPACT, K_MD5 = range(5)
-KERNEL_NAMES = ["encode", "encode_tail", "scan", "compact", "md5"]
+K_ANALYZE, K_ANALYZE_TAIL, K_SCAN, K_PACK, K_MD5 = range(5)
+KERNEL_NAMES = ["analyze", "analyze_tail", "scan", "pack", "md5"]
 
 
 class FlacGpuError(RuntimeError):
