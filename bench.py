@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--frames", type=int, default=32768, help="4096-sample blocks per GPU")
-    p.add_argument("--streams", type=int, default=1024, help="independent streams (files) per GPU")
+    p.add_argument("--streams", type=int, default=4096, help="independent streams (files) per GPU")
     p.add_argument("--channels", type=int, default=2)
     p.add_argument("--bits", type=int, default=16)
     p.add_argument("--rate", type=int, default=44100)

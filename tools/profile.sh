@@ -1,19 +1,22 @@
 #!/bin/bash
 # rocprofv3 passes over bench.py (run on the GPU box from the repo root).
-# Usage: tools/profile.sh <tag> [bench args...]
-# Writes gpurun_out/prof_<tag>/...; kernel trace + stats first, then PMC passes
-# (one counter group per pass, never combined with tracing domains).
+# Usage: tools/profile.sh <tag> <frames> [bench args...]
+# Writes gpurun_out/prof_<tag>/...: kernel trace + stats first, then PMC passes
+# (one counter group per pass, never combined with tracing domains), then
+# profiles/<tag>_summary.md + profiles/<tag>_pmc.json via tools/pmc_summary.py.
 set -e
 TAG=${1:-r1}; shift || true
-ARGS="$@"
+FRAMES=${1:-32768}; shift || true
+ARGS="--frames $FRAMES $@"
 REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $REPO/bench.py --no-cpu $ARGS > $OUT/kt.log 2>&1
 i=0
-for PMC in ${PMCS:-"FETCH_SIZE" "WRITE_SIZE"} "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
+for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/pmc$i -o pmc -- python3 $REPO/bench.py --no-cpu $ARGS > $OUT/pmc$i.log 2>&1
 done
-echo done
+cd $REPO
+python3 tools/pmc_summary.py $OUT $TAG $FRAMES
