@@ -70,7 +70,7 @@ struct flacgpu_ctx {
     hipStream_t stream = nullptr, aux = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr, *d_crc_join = nullptr;
-    uint32_t *d_err = nullptr;
+    uint32_t *d_err = nullptr, *d_ctr = nullptr;
     FrameJob *d_jobs = nullptr;
     uint8_t *d_desc = nullptr;
     uint32_t *d_fbytes = nullptr;
@@ -210,6 +210,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.out = d_out;
     a.out_cap = out_cap;
     a.err = c->d_err;
+    a.work_ctr = c->d_ctr;
     a.crc_tab = c->d_crc_tab;
     a.crc_pow = c->d_crc_pow;
     a.crc_join = c->d_crc_join;
@@ -375,14 +376,14 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     c->pcm_cap = F * (uint64_t)kBlock * c->C * c->B + 64;
     c->out_cap = F * (uint64_t)c->image_bytes;
     if (hipMalloc(&c->d_crc_tab, 1024 * 2) || hipMalloc(&c->d_crc_pow, pw.size() * 2) ||
-        hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) ||
+        hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) || hipMalloc(&c->d_ctr, 16) ||
         hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_desc, F * (uint64_t)c->desc_stride) ||
         hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
         hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16) || hipMalloc(&c->d_stamps, 32 * 8))
         return fail(FLACGPU_ERR_OUT_OF_MEMORY);
     if (hipMemcpy(c->d_crc_tab, tab.data(), 2048, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_pow, pw.data(), pw.size() * 2, hipMemcpyHostToDevice) ||
-        hipMemcpy(c->d_crc_join, pj.data(), pj.size() * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) ||
+        hipMemcpy(c->d_crc_join, pj.data(), pj.size() * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) || hipMemset(c->d_ctr, 0, 16) ||
         hipMemset(c->d_stamps, 0, 32 * 8))
         return fail(FLACGPU_ERR_DEVICE);
     flacgpu_md5_init(c);
@@ -400,6 +401,7 @@ void flacgpu_close(flacgpu_ctx *c) {
     hipFree(c->d_crc_pow);
     hipFree(c->d_crc_join);
     hipFree(c->d_err);
+    hipFree(c->d_ctr);
     hipFree(c->d_jobs);
     hipFree(c->d_desc);
     hipFree(c->d_fbytes);

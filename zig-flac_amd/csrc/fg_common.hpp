@@ -97,6 +97,8 @@ struct EncodeArgs {
     const uint64_t *offsets;    // [slot] byte offset of the frame in out (scan)
     uint8_t *out;               // contiguous output bitstream
     uint64_t out_cap;
+    uint32_t *work_ctr;         // 4 frame-queue tickets: analysis full/tail, pack full/tail (each
+                                // kernel zeroes the other stage's pair for its next launch)
     uint32_t *err;              // device error word (0 = ok; bit 0 invariant, bit 1 output too small)
     const uint16_t *crc_tab;    // 4 x 256: z^40, z^32, z^24, z^16 byte tables (CRC-16/UMTS)
     const uint16_t *crc_pow;    // [(H-1)*pack_threads + t] = z^(64*H*(T-1-t)) mod P, H = 1..crc_hmax

@@ -467,10 +467,32 @@ __device__ __forceinline__ void load_candidate(const uint32_t *stg, uint32_t cst
         fill([&](int j, uint32_t c) -> int64_t { return (int32_t)(c ? p2[j].y : p2[j].x); },
              [&](int j) -> int64_t { return (int32_t)p2[j].y; });
     } else if constexpr (NC == 2 && B == 2 && !FG_NARROW) {
-        // (L,R) packed in one dword per sample (16-B pad: conflict-free ds_read_b128)
-        const uint32_t *p1 = lw;
-        fill([&](int j, uint32_t c) -> int64_t { return c ? ((int32_t)p1[j] >> 16) : ((int32_t)(p1[j] << 16) >> 16); },
-             [&](int j) -> int64_t { return (int32_t)p1[j] >> 16; });
+        // (L,R) packed in one dword per sample, read as explicit ds_read_b128 (the 16-B pad
+        // makes a quarter-wave's 16 lanes cover all 64 banks)
+        const uint4 *q4 = (const uint4 *)lw;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            uint32_t raw[16];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint4 v = q4[4 * g + t];
+                raw[4 * t] = v.x; raw[4 * t + 1] = v.y; raw[4 * t + 2] = v.z; raw[4 * t + 3] = v.w;
+            }
+            auto put = [&](auto f) {
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    const int j = 16 * g + jj;
+                    int32_t x = f((int32_t)(raw[jj] << 16) >> 16, (int32_t)raw[jj] >> 16);
+                    if (!FULL && l * 64u + j >= n) x = 0;
+                    s[j] = (ST)x;
+                }
+            };
+            if (kind == 0 && chan == 0) put([](int32_t L, int32_t) { return L; });
+            else if (kind <= 1) put([](int32_t, int32_t R) { return R; });
+            else if (kind == 2) put([](int32_t L, int32_t R) { return (L + R) >> 1; });
+            else put([](int32_t L, int32_t R) { return L - R; });
+            __builtin_amdgcn_sched_barrier(0);
+        }
     } else {
         const uint8_t *base = (const uint8_t *)lw;
         const uint32_t CB = C * B;
@@ -551,12 +573,17 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
     uint64_t tprev_ = __builtin_amdgcn_s_memtime();
 #endif
 
-    // Persistent loop: this workgroup analyses frames blockIdx.x, +gridDim.x, ...; with double
-    // buffering the next frame's PCM is DMA'd into the idle staging buffer meanwhile.
+    // Persistent loop over a dynamic frame queue: workgroup b starts with frame b, then takes
+    // gridDim.x + (an atomic ticket) -- slower CUs (e.g. sharing SIMDs with the MD5 waves)
+    // simply take fewer frames.  With double buffering the next frame's PCM is DMA'd into
+    // the idle staging buffer while this one is analysed.
+    uint32_t *ctr = a.work_ctr + (FULL ? 0u : 1u);
+    if (blockIdx.x == 0 && tid == 0) a.work_ctr[2] = a.work_ctr[3] = 0u;  // the pack kernel's queues
     uint32_t jidx = blockIdx.x, buf = 0;
     if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, a.jobs[jidx].pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0);
-    for (; jidx < a.n_jobs; jidx += gridDim.x, buf ^= 1u) {
+    while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
+        if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
         const FrameJob job = a.jobs[jidx];
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.stage1 : LY.stage0));
@@ -565,9 +592,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
         if (dbuf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
         __syncthreads();
-        if (dbuf && jidx + gridDim.x < a.n_jobs)
-            stage_dma(a.pcm, a.jobs[jidx + gridDim.x].pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)),
-                      cw, cst, wave, NW, l);
+        const uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        if (dbuf && nxt < a.n_jobs)
+            stage_dma(a.pcm, a.jobs[nxt].pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave,
+                      NW, l);
         STAMP(0);
 
         // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
@@ -1059,6 +1087,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
         }
         __syncthreads();  // params / records / scratch are reused by the next frame
         STAMP(6);
+        jidx = nxt;
+        buf ^= 1u;
     }  // persistent frame loop
 #ifdef FG_STAMPS
     if (l == 0 && a.stamps)
@@ -1093,8 +1123,11 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL) ? FG_PACK_MINW : 2)
     for (uint32_t i = tid; i < 1024u; i += NT) crct[i] = a.crc_tab[i];
     const bool stereo = a.stereo != 0;
 
-    for (uint32_t jidx = blockIdx.x; jidx < a.n_jobs; jidx += gridDim.x) {
+    uint32_t *ctr = a.work_ctr + (FULL ? 2u : 3u);
+    if (blockIdx.x == 0 && tid == 0) a.work_ctr[0] = a.work_ctr[1] = 0u;  // the analysis kernel's queues
+    for (uint32_t jidx = blockIdx.x, nxt = 0; jidx < a.n_jobs; jidx = nxt) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
+        if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
         const FrameJob job = a.jobs[jidx];
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
         const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
@@ -1103,16 +1136,19 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL) ? FG_PACK_MINW : 2)
         const uint32_t total_bits = F->total_bits;
         const uint32_t fbytes = ((total_bits + 7u) >> 3) + 2u;
         const uint64_t D = a.offsets[job.slot];
-        if (fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap) {  // uniform: skip the frame
-            if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
-            continue;
-        }
+        const bool skip = fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap;  // uniform
         const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
                        method = sd->method, cand = sd->cand;
 
         // ---- 1. PCM -> LDS, candidate samples -> VGPRs
         stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
         __syncthreads();
+        nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        if (skip) {
+            if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
+            __syncthreads();
+            continue;
+        }
         ST s[64];
         load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, s);  // (unused for CONSTANT)
         // lane offsets from the measured segment lengths (uniform prefix of earlier subframes)
