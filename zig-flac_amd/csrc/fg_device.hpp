@@ -43,6 +43,14 @@ __device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t acc
     return d;
 }
 
+// a + b that the optimiser cannot reassociate: a long `acc += x_j` chain over an
+// unrolled loop is otherwise rebuilt as an add tree that keeps every x_j live.
+__device__ __forceinline__ uint32_t add_chain(uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_add_u32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+
 enum : int {
     DPP_XOR1 = 0xB1,     // quad_perm [1,0,3,2]
     DPP_XOR2 = 0x4E,     // quad_perm [2,3,0,1]
@@ -501,6 +509,46 @@ __device__ __forceinline__ void load_candidate(const uint32_t *stg, uint32_t cst
     }
 }
 
+// Fixed-predictor residual of order K from sample x and history q1..q4
+// (fixed.zig:12-18 COEFF_SCALAR stencil): wrapping i32 (narrow, fixed.zig:63-68)
+// or exact i64 truncated to i32 (wide, fixed.zig:69-74).
+template <int K, typename ST>
+__device__ __forceinline__ ST fixed_residual(ST x, ST q1, ST q2, ST q3, ST q4) {
+    using UT = typename std::conditional<sizeof(ST) == 4, uint32_t, uint64_t>::type;
+    const UT ux = (UT)x, u1 = (UT)q1, u2 = (UT)q2, u3 = (UT)q3, u4 = (UT)q4;
+    UT r;
+    if constexpr (K == 0) r = ux;
+    else if constexpr (K == 1) r = ux - u1;
+    else if constexpr (K == 2) r = (ux + u2) - 2u * u1;
+    else if constexpr (K == 3) r = (ux - u3) + 3u * (u2 - u1);
+    else r = (ux + u4) - 4u * (u1 + u3) + 6u * u2;
+    return (ST)(int32_t)(uint32_t)r;
+}
+
+// Residuals of a compile-time order K, read-only over s: f(j, warm, r) sees
+// every residual (lane 0's first K samples are warm-ups).  Used where the
+// residuals are consumed on the fly, so the five instantiations behind a
+// uniform switch share no live state but the caller's accumulators.
+template <int K, typename ST, typename F>
+__device__ __forceinline__ void residuals_k(const ST (&s)[64], ST h1, ST h2, ST h3, ST h4, uint32_t l, F &&f) {
+    ST q1 = h1, q2 = h2, q3 = h3, q4 = h4;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const ST x = s[j];
+        const ST r = fixed_residual<K, ST>(x, q1, q2, q3, q4);
+        q4 = q3; q3 = q2; q2 = q1; q1 = x;
+        f(j, (j < K) && (l == 0), r);
+    }
+}
+#define FG_DISPATCH_K(k, CALL)                        \
+    switch (k) {                                      \
+        case 0: { constexpr int K = 0; CALL; } break; \
+        case 1: { constexpr int K = 1; CALL; } break; \
+        case 2: { constexpr int K = 2; CALL; } break; \
+        case 3: { constexpr int K = 3; CALL; } break; \
+        default: { constexpr int K = 4; CALL; } break; \
+    }
+
 // Fixed-predictor residuals in place, s[j] := e_k (lane 0 keeps its k warm-up
 // samples; history h1..h4 = the 4 samples before the lane's chunk), for a runtime
 // (wave-uniform) order k: the difference chain
@@ -752,7 +800,6 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
         }
         STAMP(3);
 
-        uint32_t seg = 0;  // exact bits of this lane's segment of the candidate subframe
         if (try_fixed) {
             // ---- 6. residuals in place and the finest-level partition sums (rice.zig:288-340)
             SumT S8[4] = {0, 0, 0, 0};
@@ -793,7 +840,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                         }
                     }
                 };
-                residuals_generic<ST>(s, h1, h2, h3, h4, l, k, acc);
+                FG_DISPATCH_K(k, (residuals_k<K, ST>(s, h1, h2, h3, h4, l, acc)))
             }
             STAMP(4);
 
@@ -928,67 +975,15 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                 R.order = k;
                 R.porder = best_o;
                 R.method = best_m;
-                // ---- 9a. exact bits of the lane's segment (frame_writer.zig:299-372).  The
-                // residuals were not kept through the search (register pressure): reload the
-                // samples from the staged PCM and recompute them.
-                const uint32_t o = best_o, param_len = 4u + best_m, w = R.waste;
-                const uint8_t *pp = par + ((1u << o) - 1u);
-                if (l == 0) {
-                    const uint32_t p0 = pp[0];
-                    seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
-                }
-                load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, s);
-                if (w != 0) {
-#pragma unroll
-                    for (int j = 0; j < 64; j++) s[j] >>= w;
-                }
-                const ST g1 = shr1(s[63]), g2 = shr1(s[62]), g3 = shr1(s[61]), g4 = shr1(s[60]);
-                if constexpr (FULL) {
-                    const uint32_t sh = 12u - o, psz = 4096u >> o;
-                    uint32_t pq[4];
-#pragma unroll
-                    for (int q = 0; q < 4; q++) pq[q] = pp[(l * 64u + 16u * q) >> sh];
-                    auto len_a = [&](int j, bool warm, ST r) {
-                        const uint32_t p = pq[j >> 4];
-                        const bool esc = (p & 0x80u) != 0;
-                        const uint32_t i = l * 64u + j;
-                        if ((j & 15) == 0 && i != 0 && (i & (psz - 1u)) == 0) seg += param_len + (esc ? 5u : 0u);
-                        const uint32_t zz = zigzag32((int32_t)r);
-                        const uint32_t cl = esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
-                        seg += warm ? 0u : cl;
-                    };
-                    residuals_generic<ST>(s, g1, g2, g3, g4, l, k, len_a);
-                } else {
-                    const uint32_t psz = n >> o;
-                    auto len_a = [&](int j, bool warm, ST r) {
-                        const uint32_t i = l * 64u + j;
-                        if (i < n && !warm) {
-                            const uint32_t p = pp[i / psz];
-                            const bool esc = (p & 0x80u) != 0;
-                            if (i != 0 && (i % psz) == 0) seg += param_len + (esc ? 5u : 0u);
-                            const uint32_t zz = zigzag32((int32_t)r);
-                            seg += esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
-                        }
-                    };
-                    residuals_generic<ST>(s, g1, g2, g3, g4, l, k, len_a);
-                }
             }
         }
-        if (R.type == 0) {
-            seg = (l == 0) ? 8u + bd : 0u;
-        } else if (R.type == 1) {
-            const uint32_t cnt = FULL ? 64u : (n > l * 64u ? min(64u, n - l * 64u) : 0u);
-            seg = cnt * bps + ((l == 0) ? 8u + R.waste : 0u);
-        }
-        const uint32_t sub_bits = wave_sum32(seg);
         STAMP(5);
 
-        // ---- 10. publish the candidate record; stereo decision (encoder.zig:441-452)
-        // or independent channels (:456-475)
+        // ---- 9. publish the estimate; stereo decision (encoder.zig:441-452) or independent
+        // channels (:456-475)
         if (l == 0) {
             uint32_t *rc = recs + cand * 16u;
             rc[6] = (uint32_t)R.est; rc[7] = (uint32_t)(R.est >> 32);
-            rc[8] = sub_bits;
         }
         __syncthreads();
         uint32_t channel_code, n_out;
@@ -1008,13 +1003,83 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
             const uint32_t c1 = (b == 0 || b == 2) ? 1u : 3u;
             my_slot = (cand == c0) ? 0 : ((cand == c1) ? 1 : -1);
             n_out = 2;
-            misc[8] = c0;
-            misc[9] = c1;
         } else {
             channel_code = C - 1u;
             n_out = C;
             my_slot = (int)cand;
         }
+
+        if (tid == 0) {  // frame header (frame_writer.zig:151-265) while the other waves measure
+            uint32_t *hw = misc + 32;
+            hw[0] = hw[1] = hw[2] = hw[3] = 0;
+            misc[18] = write_frame_header(hw, job.number, a.bits, channel_code, n, a.sample_rate);
+        }
+
+        // ---- 10. exact bits of each lane's segment of the written subframes (pass A of
+        // frame_writer.zig:269-372).  FIXED: the residuals were not kept through the search
+        // (register pressure), so the samples are reloaded from the staged PCM.
+        uint32_t seg = 0;
+        if (my_slot >= 0) {
+            if (R.type == 0) {
+                seg = (l == 0) ? 8u + bd : 0u;
+            } else if (R.type == 1) {
+                const uint32_t cnt = FULL ? 64u : (n > l * 64u ? min(64u, n - l * 64u) : 0u);
+                seg = cnt * bps + ((l == 0) ? 8u + R.waste : 0u);
+            } else {
+                k = R.order;
+                // ---- 9a. exact bits of the lane's segment (frame_writer.zig:299-372).  The
+                // residuals were not kept through the search (register pressure): reload the
+                // samples from the staged PCM and recompute them.
+                const uint32_t o = R.porder, param_len = 4u + R.method, w = R.waste;
+                const uint8_t *pp = par + ((1u << o) - 1u);
+                if (l == 0) {
+                    const uint32_t p0 = pp[0];
+                    seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
+                }
+                ST t[64];
+                load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, t);
+                if (w != 0) {
+#pragma unroll
+                    for (int j = 0; j < 64; j++) t[j] >>= w;
+                }
+                const ST g1 = shr1(t[63]), g2 = shr1(t[62]), g3 = shr1(t[61]), g4 = shr1(t[60]);
+                if constexpr (FULL) {
+                    const uint32_t sh = 12u - o, psz = 4096u >> o;
+                    uint32_t pq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) pq[q] = pp[(l * 64u + 16u * q) >> sh];
+                    uint32_t sg[2] = {seg, 0u};  // two interleaved chains
+                    auto len_a = [&](int j, bool warm, ST r) {
+                        const uint32_t p = pq[j >> 4];
+                        const bool esc = (p & 0x80u) != 0;
+                        const uint32_t i = l * 64u + j;
+                        if ((j & 15) == 0 && i != 0 && (i & (psz - 1u)) == 0)
+                            sg[1] = add_chain(sg[1], param_len + (esc ? 5u : 0u));
+                        const uint32_t zz = zigzag32((int32_t)r);
+                        const uint32_t cl = esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
+                        sg[j & 1] = add_chain(sg[j & 1], warm ? 0u : cl);
+                    };
+                    FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, len_a)))
+                    seg = sg[0] + sg[1];
+                } else {
+                    const uint32_t psz = n >> o;
+                    auto len_a = [&](int j, bool warm, ST r) {
+                        const uint32_t i = l * 64u + j;
+                        if (i < n && !warm) {
+                            const uint32_t p = pp[i / psz];
+                            const bool esc = (p & 0x80u) != 0;
+                            if (i != 0 && (i % psz) == 0) seg += param_len + (esc ? 5u : 0u);
+                            const uint32_t zz = zigzag32((int32_t)r);
+                            seg += esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
+                        }
+                    };
+                    FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, len_a)))
+                }
+            }
+        }
+        const uint32_t sub_bits = wave_sum32(seg);
+        if (l == 0 && my_slot >= 0) misc[40 + my_slot] = sub_bits;
+        STAMP(7);
 
         // ---- 11. the frame descriptor
         uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
@@ -1038,14 +1103,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                 for (uint32_t j = l; j < np; j += 64) sd->params[j] = pp[j];
             }
         }
+        __syncthreads();  // every written wave's sub_bits
         if (tid == 0) {
-            uint32_t *hw = misc + 32;
-            hw[0] = hw[1] = hw[2] = hw[3] = 0;
-            const uint32_t hb = write_frame_header(hw, job.number, a.bits, channel_code, n, a.sample_rate);
+            const uint32_t *hw = misc + 32;
+            const uint32_t hb = misc[18];
             uint32_t total = 8u * hb;
-            if (stereo) total += recs[misc[8] * 16 + 8] + recs[misc[9] * 16 + 8];
-            else
-                for (uint32_t c = 0; c < C; c++) total += recs[c * 16 + 8];
+            for (uint32_t c = 0; c < n_out; c++) total += misc[40 + c];
             FrameDesc *f = (FrameDesc *)fd;
             f->hdr_bytes = hb;
             f->total_bits = total;
@@ -1060,7 +1123,6 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
 
         // ---- 12. optional decision records (parity tests)
         if (a.records) {
-            __syncthreads();
             FrameRec *fr = a.records + job.slot;
             SubRec *sr = &fr->cand[cand];
             if (l == 0) {
