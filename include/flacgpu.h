@@ -132,6 +132,59 @@ int flacgpu_encode_plan_device(flacgpu_ctx *ctx, const flacgpu_plan *plan, const
                                uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets,
                                uint64_t *d_total, uint8_t *d_md5, void *hip_stream);
 
+/* ---- File level (host code around the GPU frame path) --------------------- */
+
+/* The context's configuration (what flacgpu_open was given). */
+int flacgpu_get_config(const flacgpu_ctx *ctx, flacgpu_config *out);
+
+/* WavReader.init / getFmt (wav_reader.zig:116-170) and the flacStreaminfo checks
+ * (wav_reader.zig:92-108) on an in-memory WAV file: the PCM data chunk starts at
+ * data_offset; samples = data_len / (channels * (bits/8)) as in wav_reader.zig:169. */
+typedef struct {
+    uint32_t sample_rate;
+    uint16_t channels;
+    uint16_t bits_per_sample;   /* valid bits (EXTENSIBLE) or the fmt bit depth */
+    uint16_t bytes_per_sample;  /* block_align / channels */
+    uint16_t pad;
+    uint64_t samples;           /* interchannel samples */
+    uint64_t data_offset;
+    uint64_t data_bytes;
+} flacgpu_wav_info;
+int flacgpu_wav_parse(const void *wav, size_t len, flacgpu_wav_info *info);
+
+/* StreamInfo (metadata.zig:18-68). */
+typedef struct {
+    uint8_t md5[16];
+    uint64_t interchannel_samples;
+    uint32_t min_frame_size;    /* u24; starts at 0xFFFFFF */
+    uint32_t max_frame_size;    /* u24; starts at 0 */
+    uint32_t sample_rate;
+    uint16_t min_block_size;
+    uint16_t max_block_size;
+    uint8_t channels;
+    uint8_t bit_depth;
+    uint8_t pad[6];
+} flacgpu_streaminfo;
+void flacgpu_streaminfo_init(flacgpu_streaminfo *si, uint32_t sample_rate, uint32_t channels, uint32_t bit_depth,
+                             uint64_t interchannel_samples, uint32_t block_size);
+/* StreamInfo.updateFrameSize (metadata.zig:35-40), with its else-if. */
+void flacgpu_streaminfo_update_frame_size(flacgpu_streaminfo *si, uint32_t frame_size);
+/* StreamInfo.bytes (metadata.zig:42-68). */
+void flacgpu_streaminfo_bytes(const flacgpu_streaminfo *si, uint8_t out[34]);
+/* Encoder.writeHeader (encoder.zig:192-206): "fLaC" + STREAMINFO block; returns 42. */
+size_t flacgpu_header_bytes(const flacgpu_streaminfo *si, int last_metadata, uint8_t out[42]);
+/* Encoder.writeVorbisComment (encoder.zig:211-226): vendor "toastori FLAC 0.0.0", no tags; returns 31. */
+size_t flacgpu_vorbis_comment_bytes(int last_metadata, uint8_t out[31]);
+
+/* wav2flac (wav2flac.zig:10-97) for PCM in memory: the 73-byte header (STREAMINFO not
+ * last, VORBIS_COMMENT last) + every frame, STREAMINFO carrying the frame-size
+ * min/max and the MD5 of the PCM bytes (both computed on the GPU). */
+int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
+                        uint8_t *out, size_t out_cap, size_t *out_len);
+/* The whole conversion of an in-memory WAV file on HIP device `device`
+ * (Config.default for the WAV's channels and bit depth). */
+int flacgpu_wav_to_flac(int device, const void *wav, size_t wav_len, uint8_t *out, size_t out_cap, size_t *out_len);
+
 /* ---- Instrumentation ---------------------------------------------------- */
 /* Kernel ids for flacgpu_kernel_time: frame analysis (4096-sample frames /
  * short frames), frame-size scan, frame packing (all frames), stream MD5. */

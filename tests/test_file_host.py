@@ -1,0 +1,174 @@
+"""File-level host code of libflacgpu.so (fg_file.cpp): WAV header parsing,
+StreamInfo, the metadata writers, and (GPU) whole-file encodes, against the
+restatement's oracle_encode_file (wav2flac.zig:10-97, metadata.zig, encoder.zig:177-226)."""
+import ctypes
+import hashlib
+import io
+import struct
+import wave
+
+import numpy as np
+import pytest
+
+import flacgpu
+import oracle_ref
+import synth
+
+
+def make_wav(pcm: bytes, ch: int, bits: int, rate: int) -> bytes:
+    b = io.BytesIO()
+    with wave.open(b, "wb") as w:
+        w.setnchannels(ch)
+        w.setsampwidth(bits // 8)
+        w.setframerate(rate)
+        w.writeframes(pcm)
+    return b.getvalue()
+
+
+def make_wav_extensible(pcm: bytes, ch: int, bits: int, rate: int, valid_bits: int, junk: bool = True) -> bytes:
+    B = bits // 8
+    fmt = struct.pack("<HHIIHH", 0xFFFE, ch, rate, rate * ch * B, ch * B, bits)
+    fmt += struct.pack("<HHI", 22, valid_bits, 0) + b"\x01\x00\x00\x00\x00\x00\x10\x00\x80\x00\x00\xaa\x00\x38\x9b\x71"
+    chunks = b""
+    if junk:
+        chunks += b"JUNK" + struct.pack("<I", 6) + b"\x00" * 6
+    chunks += b"fmt " + struct.pack("<I", len(fmt)) + fmt
+    if junk:
+        chunks += b"LIST" + struct.pack("<I", 4) + b"INFO"
+    chunks += b"data" + struct.pack("<I", len(pcm)) + pcm
+    return b"RIFF" + struct.pack("<I", 4 + len(chunks)) + b"WAVE" + chunks
+
+
+@pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (1, 24, 96000), (8, 32, 48000), (3, 8, 22050)])
+def test_wav_parse_plain(ch, bits, rate):
+    pcm = synth.synth_pcm(1000, ch, bits, rate)
+    w = make_wav(pcm, ch, bits, rate)
+    info = flacgpu.wav_parse(w)
+    assert (info.channels, info.bits_per_sample, info.sample_rate, info.samples) == (ch, bits, rate, 1000)
+    assert w[info.data_offset:info.data_offset + info.data_bytes] == pcm
+
+
+def test_wav_parse_extensible_and_chunks():
+    pcm = synth.synth_pcm(333, 2, 24, 96000)
+    w = make_wav_extensible(pcm, 2, 24, 96000, 24)
+    info = flacgpu.wav_parse(w)
+    assert (info.channels, info.bits_per_sample, info.bytes_per_sample, info.samples) == (2, 24, 3, 333)
+    assert w[info.data_offset:info.data_offset + info.data_bytes] == pcm
+
+
+@pytest.mark.parametrize("mutate", ["riff", "wave", "codec", "byterate", "datalen", "nodata"])
+def test_wav_parse_rejects(mutate):
+    pcm = synth.synth_pcm(100, 2, 16, 44100)
+    w = bytearray(make_wav(pcm, 2, 16, 44100))
+    if mutate == "riff":
+        w[0:4] = b"RIFX"
+    elif mutate == "wave":
+        w[8:12] = b"AVI "
+    elif mutate == "codec":
+        w[20:22] = struct.pack("<H", 3)  # IEEE float
+    elif mutate == "byterate":
+        w[28:32] = struct.pack("<I", 1)
+    elif mutate == "datalen":
+        w[40:44] = struct.pack("<I", len(pcm) - 1)
+    elif mutate == "nodata":
+        w[36:40] = b"dat_"
+    with pytest.raises(flacgpu.FlacGpuError):
+        flacgpu.wav_parse(bytes(w))
+
+
+def test_streaminfo_update_quirk_and_bytes():
+    si = flacgpu.StreamInfo.new(44100, 2, 16, 123456)
+    si.update_frame_size(1000)   # raises max only: min stays 0xFFFFFF
+    assert (si.min_frame_size, si.max_frame_size) == (0xFFFFFF, 1000)
+    si.update_frame_size(900)    # below max: lowers min
+    si.update_frame_size(1200)
+    si.update_frame_size(950)
+    assert (si.min_frame_size, si.max_frame_size) == (900, 1200)
+    b = si.bytes()
+    assert b[0:4] == bytes([0x10, 0x00, 0x10, 0x00])
+    assert b[4:7] == (900).to_bytes(3, "big") and b[7:10] == (1200).to_bytes(3, "big")
+    packed = int.from_bytes(b[10:18], "big")
+    assert packed >> 44 == 44100 and (packed >> 41) & 7 == 1 and (packed >> 36) & 31 == 15
+    assert packed & ((1 << 36) - 1) == 123456
+
+
+@pytest.mark.parametrize("ch,bits,rate,n", [(2, 16, 44100, 2 * 4096 + 333), (1, 24, 96000, 4096),
+                                             (2, 32, 192000, 5000), (8, 24, 96000, 100)])
+def test_header_bytes_match_oracle_file(ch, bits, rate, n):
+    pcm = synth.synth_pcm(n, ch, bits, rate)
+    ref = oracle_ref.encode_file(pcm, ch, bits, rate)
+    _, sizes, md5 = oracle_ref.encode_stream(pcm, ch, bits, rate)
+    si = flacgpu.StreamInfo.new(rate, ch, bits, n)
+    for s in sizes:
+        si.update_frame_size(s)
+    ctypes.memmove(si.md5, hashlib.md5(pcm).digest(), 16)
+    hdr = flacgpu.header_bytes(si, False) + flacgpu.vorbis_comment_bytes(True)
+    assert len(hdr) == 73 and hdr == ref[:73]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ch,bits,rate,n", [(2, 16, 44100, 3 * 4096 + 1000), (1, 16, 44100, 4096),
+                                             (2, 24, 96000, 2 * 4096 + 7), (2, 32, 192000, 4096 + 1),
+                                             (8, 24, 96000, 4096 + 100), (2, 16, 44100, 1)])
+def test_gpu_encode_file_matches_oracle(ch, bits, rate, n):
+    pcm = synth.synth_pcm(n, ch, bits, rate)
+    with flacgpu.Encoder(ch, bits, rate, max_frames=16) as enc:
+        out = enc.encode_file(pcm)
+    assert out == oracle_ref.encode_file(pcm, ch, bits, rate)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (2, 24, 96000), (1, 32, 48000)])
+def test_gpu_wav_to_flac(ch, bits, rate):
+    n = 2 * 4096 + 77
+    pcm = synth.synth_pcm(n, ch, bits, rate)
+    out = flacgpu.wav_to_flac(make_wav(pcm, ch, bits, rate))
+    assert out == oracle_ref.encode_file(pcm, ch, bits, rate)
+    dec, _ = oracle_ref.decode_frames(out[73:], ch, bits, rate, n)
+    assert dec == pcm and out[8 + 18:8 + 34] == hashlib.md5(pcm).digest()
+
+
+CPP_DIR = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "cpp")
+
+
+def _cpp_driver():
+    import os
+    import subprocess
+
+    subprocess.check_call(["make", "-s", "-C", CPP_DIR])
+    return os.path.join(CPP_DIR, "build", "encoder_api_test")
+
+
+def _has_gpu():
+    try:
+        import torch
+
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-device failure path")
+def test_cpp_api_driver_builds_and_fails_loudly_without_gpu(tmp_path):
+    import subprocess
+
+    exe = _cpp_driver()
+    raw = tmp_path / "x.raw"
+    raw.write_bytes(synth.synth_pcm(100, 2, 16, 44100))
+    r = subprocess.run([exe, str(raw), "2", "16", "44100", str(tmp_path / "o.flac")], capture_output=True, text=True)
+    assert r.returncode == 1 and "HIP device error" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ch,bits,rate,n", [(2, 16, 44100, 3 * 4096 + 1000), (1, 24, 96000, 4096 + 3),
+                                             (8, 16, 48000, 4096 + 64)])
+def test_cpp_encoder_api_matches_oracle_file(tmp_path, ch, bits, rate, n):
+    import subprocess
+
+    exe = _cpp_driver()
+    pcm = synth.synth_pcm(n, ch, bits, rate)
+    raw = tmp_path / "x.raw"
+    raw.write_bytes(pcm)
+    out = tmp_path / "o.flac"
+    subprocess.check_call([exe, str(raw), str(ch), str(bits), str(rate), str(out)])
+    assert out.read_bytes() == oracle_ref.encode_file(pcm, ch, bits, rate)

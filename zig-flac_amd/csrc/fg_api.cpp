@@ -300,6 +300,12 @@ const char *flacgpu_strerror(int code) {
 
 int flacgpu_abi_version(void) { return FLACGPU_ABI_VERSION; }
 
+int flacgpu_get_config(const flacgpu_ctx *c, flacgpu_config *out) {
+    if (!c || !out) return FLACGPU_ERR_INVALID_INPUT;
+    *out = c->cfg;
+    return FLACGPU_OK;
+}
+
 size_t flacgpu_reference_max_frame_bytes(const flacgpu_config *cfg) {
     if (!cfg) return 0;
     // maxFrameBytes(block_size, bit_depth, channels, compute_waste_bits=true) (encoder.zig:55-60,583-595)

@@ -1,0 +1,195 @@
+// fg_file.cpp -- host-side file assembly around the GPU frame encoder: WAV
+// header parsing (WavReader.init/getFmt, src/lib/wav_reader.zig:92-170),
+// StreamInfo (src/lib/metadata.zig:18-68), the metadata writers of the
+// reference Encoder (skipHeader/writeHeader/writeVorbisComment,
+// src/lib/encoder.zig:177-226) and the wav2flac driver
+// (src/cli/wav2flac.zig:10-97).  Pure host code: every sample goes through the
+// GPU kernels via flacgpu_encode_frames; only the 73 metadata bytes are built
+// here.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/flacgpu.h"
+
+namespace {
+
+constexpr char kVendor[] = "toastori FLAC 0.0.0";  // encoder.zig:212
+constexpr uint32_t kVendorLen = sizeof(kVendor) - 1;
+
+uint32_t rd_le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
+uint16_t rd_le16(const uint8_t *p) { return (uint16_t)(p[0] | p[1] << 8); }
+void wr_be(uint8_t *p, uint64_t v, int n) {
+    for (int i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * (n - 1 - i)));
+}
+
+}  // namespace
+
+extern "C" {
+
+// WavReader.init + getFmt (wav_reader.zig:116-170) + flacStreaminfo checks (:92-108).
+int flacgpu_wav_parse(const void *wav, size_t len, flacgpu_wav_info *info) {
+    if (!wav || !info) return FLACGPU_ERR_INVALID_INPUT;
+    const uint8_t *p = (const uint8_t *)wav;
+    size_t pos = 0;
+    auto need = [&](size_t n) { return pos + n <= len; };
+    if (!need(12) || std::memcmp(p, "RIFF", 4) || std::memcmp(p + 8, "WAVE", 4)) return FLACGPU_ERR_INVALID_INPUT;
+    pos = 12;
+    // skip chunks until "fmt " (wav_reader.zig:125-128)
+    for (;;) {
+        if (!need(8)) return FLACGPU_ERR_INVALID_INPUT;
+        if (!std::memcmp(p + pos, "fmt ", 4)) break;
+        pos += 8 + rd_le32(p + pos + 4);
+    }
+    pos += 8;  // tag + fmt size (the size field is not used, as in the reference)
+    if (!need(16)) return FLACGPU_ERR_INVALID_INPUT;
+    const uint16_t codec = rd_le16(p + pos);
+    if (codec != 1 && codec != 0xFFFE) return FLACGPU_ERR_INVALID_CONFIG;  // UnsupportCodec
+    const uint32_t channels = rd_le16(p + pos + 2);
+    const uint32_t rate = rd_le32(p + pos + 4);
+    const uint32_t byte_rate = rd_le32(p + pos + 8);
+    const uint32_t block_align = rd_le16(p + pos + 12);
+    uint32_t bit_depth = rd_le16(p + pos + 14);
+    pos += 16;
+    if (bit_depth < 4 || bit_depth > 32 || channels == 0) return FLACGPU_ERR_INVALID_CONFIG;
+    const uint32_t bytes_per_sample = block_align / channels;
+    if (byte_rate != rate * channels * bytes_per_sample) return FLACGPU_ERR_INVALID_INPUT;  // BitRateUnmatch
+    if (codec == 0xFFFE) {  // extension size, valid bits, channel mask, subformat
+        if (!need(24)) return FLACGPU_ERR_INVALID_INPUT;
+        bit_depth = rd_le16(p + pos + 2);
+        pos += 24;
+    }
+    for (;;) {  // skip unknown subchunks until "data"
+        if (!need(8)) return FLACGPU_ERR_INVALID_INPUT;  // DataNotFound
+        if (!std::memcmp(p + pos, "data", 4)) break;
+        pos += 8 + rd_le32(p + pos + 4);
+    }
+    const uint32_t data_len = rd_le32(p + pos + 4);
+    pos += 8;
+    if (block_align == 0 || data_len % block_align != 0) return FLACGPU_ERR_INVALID_INPUT;  // InvalidDataLen
+    if (bit_depth / 8 == 0) return FLACGPU_ERR_INVALID_CONFIG;
+    const uint64_t samples = data_len / (channels * (bit_depth / 8));  // wav_reader.zig:169
+    // flacStreaminfo (wav_reader.zig:92-108)
+    if (bit_depth < 4 || bit_depth > 32 || channels > 8 || rate >= (1u << 20) || samples >= (1ull << 36))
+        return FLACGPU_ERR_INVALID_CONFIG;
+    info->sample_rate = rate;
+    info->channels = (uint16_t)channels;
+    info->bits_per_sample = (uint16_t)bit_depth;
+    info->bytes_per_sample = (uint16_t)bytes_per_sample;
+    info->samples = samples;
+    info->data_offset = pos;
+    info->data_bytes = std::min<uint64_t>(data_len, len - pos);
+    return FLACGPU_OK;
+}
+
+// StreamInfo defaults (metadata.zig:18-33; wav_reader.zig:98-107 sets block sizes = 4096).
+void flacgpu_streaminfo_init(flacgpu_streaminfo *si, uint32_t sample_rate, uint32_t channels, uint32_t bit_depth,
+                             uint64_t interchannel_samples, uint32_t block_size) {
+    if (!si) return;
+    std::memset(si, 0, sizeof(*si));
+    si->min_frame_size = 0xFFFFFFu;
+    si->max_frame_size = 0;
+    si->sample_rate = sample_rate;
+    si->channels = (uint8_t)channels;
+    si->bit_depth = (uint8_t)bit_depth;
+    si->interchannel_samples = interchannel_samples;
+    si->min_block_size = (uint16_t)block_size;
+    si->max_block_size = (uint16_t)block_size;
+}
+
+// updateFrameSize (metadata.zig:35-40), including its else-if: a frame that raises
+// max never lowers min.
+void flacgpu_streaminfo_update_frame_size(flacgpu_streaminfo *si, uint32_t frame_size) {
+    if (!si) return;
+    frame_size &= 0xFFFFFFu;
+    if (frame_size > si->max_frame_size) si->max_frame_size = frame_size;
+    else if (frame_size < si->min_frame_size) si->min_frame_size = frame_size;
+}
+
+// StreamInfo.bytes (metadata.zig:42-68): 34 big-endian bytes.
+void flacgpu_streaminfo_bytes(const flacgpu_streaminfo *si, uint8_t out[34]) {
+    wr_be(out + 0, si->min_block_size, 2);
+    wr_be(out + 2, si->max_block_size, 2);
+    wr_be(out + 4, si->min_frame_size & 0xFFFFFFu, 3);
+    wr_be(out + 7, si->max_frame_size & 0xFFFFFFu, 3);
+    // 20-bit rate, 3-bit channels-1, 5-bit bits-1, 36-bit samples
+    const uint64_t packed = ((uint64_t)(si->sample_rate & 0xFFFFFu) << 44) |
+                            ((uint64_t)((si->channels - 1u) & 7u) << 41) |
+                            ((uint64_t)((si->bit_depth - 1u) & 31u) << 36) |
+                            (si->interchannel_samples & 0xFFFFFFFFFull);
+    wr_be(out + 10, packed, 8);
+    std::memcpy(out + 18, si->md5, 16);
+}
+
+// writeHeader (encoder.zig:192-206): "fLaC", STREAMINFO block header, 34 bytes.
+size_t flacgpu_header_bytes(const flacgpu_streaminfo *si, int last_metadata, uint8_t out[42]) {
+    std::memcpy(out, "fLaC", 4);
+    out[4] = (uint8_t)((last_metadata ? 0x80u : 0u) | 0u);  // BlockHeader{type StreamInfo}
+    wr_be(out + 5, 34, 3);
+    flacgpu_streaminfo_bytes(si, out + 8);
+    return 42;
+}
+
+// writeVorbisComment (encoder.zig:211-226): vendor string, no tags.
+size_t flacgpu_vorbis_comment_bytes(int last_metadata, uint8_t out[31]) {
+    out[0] = (uint8_t)((last_metadata ? 0x80u : 0u) | 4u);  // BlockHeader{type VorbisComment}
+    wr_be(out + 1, kVendorLen + 8, 3);
+    out[4] = (uint8_t)kVendorLen;
+    out[5] = out[6] = out[7] = 0;
+    std::memcpy(out + 8, kVendor, kVendorLen);
+    std::memset(out + 8 + kVendorLen, 0, 4);
+    return 12 + kVendorLen;
+}
+
+// wav2flac.main + encode (wav2flac.zig:10-97) for PCM already in memory: skipHeader,
+// writeVorbisComment(true), every frame through the GPU (sizes replayed into
+// updateFrameSize in frame order), MD5 on the GPU, then the header written last.
+int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
+                        uint8_t *out, size_t out_cap, size_t *out_len) {
+    if (!ctx || !out || !out_len || (!pcm && n_samples)) return FLACGPU_ERR_INVALID_INPUT;
+    *out_len = 0;
+    flacgpu_config cfg;
+    int rc = flacgpu_get_config(ctx, &cfg);
+    if (rc) return rc;
+    if (out_cap < 73) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
+    const uint64_t block = cfg.block_size;
+    const uint64_t n_frames = (n_samples + block - 1) / block;
+    std::vector<uint32_t> sizes(n_frames ? n_frames : 1);
+    size_t frames_len = 0;
+    rc = flacgpu_encode_frames(ctx, pcm, bytes_per_sample, n_samples, 0, out + 73, out_cap - 73, &frames_len,
+                               sizes.data());
+    if (rc) return rc;
+    flacgpu_streaminfo si;
+    flacgpu_streaminfo_init(&si, cfg.sample_rate, cfg.channels, cfg.bits_per_sample, n_samples, 4096);
+    for (uint64_t f = 0; f < n_frames; f++) flacgpu_streaminfo_update_frame_size(&si, sizes[f]);
+    if ((rc = flacgpu_md5_init(ctx))) return rc;
+    if ((rc = flacgpu_md5_update(ctx, pcm, (size_t)(n_samples * cfg.channels * bytes_per_sample)))) return rc;
+    if ((rc = flacgpu_md5_final(ctx, si.md5))) return rc;
+    flacgpu_header_bytes(&si, 0, out);
+    flacgpu_vorbis_comment_bytes(1, out + 42);
+    *out_len = 73 + frames_len;
+    return FLACGPU_OK;
+}
+
+// The whole wav2flac conversion of an in-memory WAV file on GPU `device`.
+int flacgpu_wav_to_flac(int device, const void *wav, size_t wav_len, uint8_t *out, size_t out_cap, size_t *out_len) {
+    if (!out_len) return FLACGPU_ERR_INVALID_INPUT;
+    *out_len = 0;
+    flacgpu_wav_info wi;
+    int rc = flacgpu_wav_parse(wav, wav_len, &wi);
+    if (rc) return rc;
+    if (wi.bytes_per_sample * 8u != wi.bits_per_sample) return FLACGPU_ERR_INVALID_CONFIG;  // container == depth only
+    // 8-bit WAV data is unsigned; the reference's 8-bit conversion is broken
+    // (wav_reader.zig:71-78), so there is no behaviour to match.
+    if (wi.bits_per_sample == 8) return FLACGPU_ERR_INVALID_CONFIG;
+    if (wi.data_bytes < wi.samples * wi.channels * wi.bytes_per_sample) return FLACGPU_ERR_INVALID_INPUT;
+    const flacgpu_config cfg = flacgpu_config_default(wi.channels, wi.bits_per_sample, wi.sample_rate);
+    flacgpu_ctx *ctx = nullptr;
+    if ((rc = flacgpu_open(device, &cfg, 0, &ctx))) return rc;
+    rc = flacgpu_encode_file(ctx, (const uint8_t *)wav + wi.data_offset, wi.bytes_per_sample, wi.samples, out, out_cap,
+                             out_len);
+    flacgpu_close(ctx);
+    return rc;
+}
+
+}  // extern "C"

@@ -83,6 +83,65 @@ class FrameRecord(ctypes.Structure):
     ]
 
 
+class WavInfo(ctypes.Structure):
+    """flacgpu_wav_info: WavReader's view of a WAV header (wav_reader.zig:116-170)."""
+    _fields_ = [("sample_rate", ctypes.c_uint32), ("channels", ctypes.c_uint16), ("bits_per_sample", ctypes.c_uint16),
+                ("bytes_per_sample", ctypes.c_uint16), ("pad", ctypes.c_uint16), ("samples", ctypes.c_uint64),
+                ("data_offset", ctypes.c_uint64), ("data_bytes", ctypes.c_uint64)]
+
+
+class StreamInfo(ctypes.Structure):
+    """flacgpu_streaminfo == metadata.StreamInfo (metadata.zig:18-33)."""
+    _fields_ = [("md5", ctypes.c_uint8 * 16), ("interchannel_samples", ctypes.c_uint64),
+                ("min_frame_size", ctypes.c_uint32), ("max_frame_size", ctypes.c_uint32),
+                ("sample_rate", ctypes.c_uint32), ("min_block_size", ctypes.c_uint16),
+                ("max_block_size", ctypes.c_uint16), ("channels", ctypes.c_uint8), ("bit_depth", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8 * 6)]
+
+    def update_frame_size(self, size: int) -> None:
+        load_library().flacgpu_streaminfo_update_frame_size(ctypes.byref(self), size)
+
+    def bytes(self) -> bytes:
+        out = ctypes.create_string_buffer(34)
+        load_library().flacgpu_streaminfo_bytes(ctypes.byref(self), out)
+        return out.raw
+
+    @classmethod
+    def new(cls, sample_rate: int, channels: int, bit_depth: int, samples: int, block_size: int = 4096):
+        si = cls()
+        load_library().flacgpu_streaminfo_init(ctypes.byref(si), sample_rate, channels, bit_depth, samples, block_size)
+        return si
+
+
+def wav_parse(wav: bytes) -> WavInfo:
+    info = WavInfo()
+    _check(load_library().flacgpu_wav_parse(wav, len(wav), ctypes.byref(info)), "wav_parse")
+    return info
+
+
+def header_bytes(si: StreamInfo, last: bool) -> bytes:
+    out = ctypes.create_string_buffer(42)
+    n = load_library().flacgpu_header_bytes(ctypes.byref(si), 1 if last else 0, out)
+    return out.raw[:n]
+
+
+def vorbis_comment_bytes(last: bool) -> bytes:
+    out = ctypes.create_string_buffer(31)
+    n = load_library().flacgpu_vorbis_comment_bytes(1 if last else 0, out)
+    return out.raw[:n]
+
+
+def wav_to_flac(wav: bytes, device: int = 0) -> bytes:
+    """wav2flac (wav2flac.zig:10-97) of an in-memory WAV file on the GPU."""
+    info = wav_parse(wav)
+    cfg = Config.default(info.channels, info.bits_per_sample, info.sample_rate)
+    cap = 200 + ((info.samples + 4095) // 4096 + 1) * load_library().flacgpu_frame_bound_bytes(ctypes.byref(cfg))
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    _check(load_library().flacgpu_wav_to_flac(device, wav, len(wav), out, cap, ctypes.byref(n)), "wav_to_flac")
+    return out.raw[: n.value]
+
+
 _lib = None
 
 
@@ -119,6 +178,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_reset_timing": (I32, [P]),
         "flacgpu_set_records": (I32, [P, I32]),
         "flacgpu_get_records": (I32, [P, P, U64, ctypes.POINTER(U64)]),
+        "flacgpu_get_config": (I32, [P, ctypes.POINTER(Config)]),
+        "flacgpu_wav_parse": (I32, [P, SZ, ctypes.POINTER(WavInfo)]),
+        "flacgpu_streaminfo_init": (None, [ctypes.POINTER(StreamInfo), U32, U32, U32, U64, U32]),
+        "flacgpu_streaminfo_update_frame_size": (None, [ctypes.POINTER(StreamInfo), U32]),
+        "flacgpu_streaminfo_bytes": (None, [ctypes.POINTER(StreamInfo), P]),
+        "flacgpu_header_bytes": (SZ, [ctypes.POINTER(StreamInfo), I32, P]),
+        "flacgpu_vorbis_comment_bytes": (SZ, [I32, P]),
+        "flacgpu_encode_file": (I32, [P, P, U32, U64, P, SZ, ctypes.POINTER(SZ)]),
+        "flacgpu_wav_to_flac": (I32, [I32, P, SZ, P, SZ, ctypes.POINTER(SZ)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -136,6 +204,9 @@ def exported_symbols() -> list:
         "flacgpu_plan_create", "flacgpu_plan_destroy", "flacgpu_plan_frames", "flacgpu_plan_out_bound",
         "flacgpu_plan_stream_first_frame", "flacgpu_encode_plan_device", "flacgpu_set_timing",
         "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_get_records",
+        "flacgpu_get_config", "flacgpu_wav_parse", "flacgpu_streaminfo_init", "flacgpu_streaminfo_update_frame_size",
+        "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file",
+        "flacgpu_wav_to_flac",
     ]
 
 
@@ -226,6 +297,19 @@ class Encoder:
         _check(self.lib.flacgpu_encode_frames(self.ctx, src, self.bytes_per_sample, n, first_frame, out, cap,
                                               ctypes.byref(out_len), sizes), "encode_frames")
         return out.raw[: out_len.value], list(sizes)[:nf]
+
+    def encode_file(self, pcm: bytes) -> bytes:
+        """Whole .flac file (73-byte header + frames) for interleaved LE PCM (wav2flac.zig:10-97)."""
+        per = self.channels * self.bytes_per_sample
+        n = len(pcm) // per
+        nf = (n + self.block_size - 1) // self.block_size
+        cap = 200 + nf * self.frame_bound()
+        out = ctypes.create_string_buffer(cap)
+        out_len = ctypes.c_size_t(0)
+        src = ctypes.create_string_buffer(bytes(pcm), len(pcm)) if pcm else None
+        _check(self.lib.flacgpu_encode_file(self.ctx, src, self.bytes_per_sample, n, out, cap, ctypes.byref(out_len)),
+               "encode_file")
+        return out.raw[: out_len.value]
 
     def write_frame(self, planes, frame_number: int) -> bytes:
         """Encoder.writeFrame: planar int32 samples (C x n) -> one frame."""
