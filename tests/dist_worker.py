@@ -1,0 +1,61 @@
+"""Worker for the multi-process tests of zig-flac_amd/parallel.py (launched by
+torch.distributed.run).  --encoder oracle: frames from the CPU restatement (test
+infrastructure standing in for the GPU, to exercise sharding + gather + file
+assembly on a CPU-only machine); --encoder gpu: flacgpu.Encoder on cuda:0.
+Rank 0 writes the assembled file to --out."""
+import argparse
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "zig-flac_amd"))
+
+
+class OracleFrames:
+    """encode_frames() of the restatement, with the attributes parallel.encode_sharded reads."""
+
+    def __init__(self, ch, bits, rate, block=4096):
+        self.channels, self.bits, self.sample_rate, self.block_size = ch, bits, rate, block
+        self.bytes_per_sample = bits // 8
+
+    def encode_frames(self, pcm, first_frame=0):
+        import oracle_ref
+
+        out, sizes, _ = oracle_ref.encode_stream(pcm, self.channels, self.bits, self.sample_rate, self.block_size,
+                                                 first_frame=first_frame)
+        return out, sizes
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--encoder", choices=["oracle", "gpu"], default="oracle")
+    p.add_argument("--channels", type=int, default=2)
+    p.add_argument("--bits", type=int, default=16)
+    p.add_argument("--rate", type=int, default=44100)
+    p.add_argument("--samples", type=int, default=10 * 4096 + 123)
+    p.add_argument("--md5", default="host")
+    p.add_argument("--out", required=True)
+    a = p.parse_args()
+    import torch.distributed as dist
+
+    import parallel
+    import synth
+
+    dist.init_process_group("gloo")
+    pcm = synth.synth_pcm(a.samples, a.channels, a.bits, a.rate)
+    if a.encoder == "gpu":
+        import flacgpu
+
+        enc = flacgpu.Encoder(a.channels, a.bits, a.rate, device=0, max_frames=256)
+    else:
+        enc = OracleFrames(a.channels, a.bits, a.rate)
+    out = parallel.encode_sharded(enc, pcm, dist=dist, device="cpu", md5=a.md5)
+    if dist.get_rank() == 0:
+        open(a.out, "wb").write(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
