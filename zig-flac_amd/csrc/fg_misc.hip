@@ -135,6 +135,9 @@ __global__ void __launch_bounds__(64) k_md5_streams(const uint8_t *base, const u
                                                     uint32_t n_streams, uint8_t *digests) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_streams) return;
+    // The chain is latency-bound (one dependent VALU op every issue slot) and these few
+    // waves share SIMDs with the encode kernels: take issue priority over them.
+    __builtin_amdgcn_s_setprio(3);
     const uint8_t *p = base + offs[s];
     const uint64_t len = lens[s];
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
