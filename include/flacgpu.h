@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FLACGPU_ABI_VERSION 1
+#define FLACGPU_ABI_VERSION 2
 
 /* Error codes (map to the Zig error set
  * {OutOfMemory, WriteFailed, DeviceError, InvalidConfig, InvalidInput}). */
@@ -51,7 +51,9 @@ typedef struct {
     uint8_t max_rice_part_order;   /* Feature.max_rice_order, 0..8 (default 8) */
     uint8_t max_rice_param;        /* Feature.max_rice_param, 1..30 (default 30) */
     uint8_t prediction;            /* Feature.prediction: 0 = fixed (the only value the
-                                      reference implements; it never reads the field) */
+                                      reference implements; it never reads the field).
+                                      Build-defined extension: 1..12 = also search LPC
+                                      orders 1..prediction (DESIGN.md "LPC") */
 } flacgpu_config;
 
 /* Config.default(channels, bit_depth) (encoder.zig:642-655). */
@@ -201,7 +203,7 @@ int flacgpu_reset_timing(flacgpu_ctx *ctx);
  * stores one flacgpu_frame_record per frame, readable with
  * flacgpu_get_records after a synchronous call. */
 typedef struct {
-    uint8_t type;       /* 0 CONSTANT, 1 VERBATIM, 2 FIXED */
+    uint8_t type;       /* 0 CONSTANT, 1 VERBATIM, 2 FIXED, 3 LPC */
     uint8_t waste;
     uint8_t bits;       /* channel bit depth before waste removal */
     uint8_t order;
@@ -213,6 +215,10 @@ typedef struct {
     uint64_t estimate;
     int64_t constant;
     uint8_t params[256];
+    uint8_t lpc_precision;  /* LPC only */
+    int8_t lpc_shift;
+    uint8_t pad3[6];
+    int32_t lpc_coefs[32];
 } flacgpu_subframe_record;
 
 typedef struct {

@@ -9,6 +9,7 @@
  */
 #include "flac_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -388,6 +389,121 @@ static void calc_residuals(const int64_t *s, uint32_t n, unsigned k, int wide, i
 }
 
 /* ===================================================================== */
+/* LPC -- build-defined extension.  The reference has no LPC (readme.md:27 */
+/* lists it as in progress; Prediction = {fixed, none}, encoder.zig:629-640;*/
+/* the `linear` subframe is commented out, encoder.zig:694-699), so this is */
+/* the contract the gfx950 kernels share with this restatement bit for bit: */
+/*  1. window w(i) = (i+1)(n-i): integer, Welch-shaped, never zero;        */
+/*  2. xw(i) = (x(i) w(i)) >> sh (arithmetic), sh = max(0, bitlen(max|x|)  */
+/*     + bitlen(floor((n+1)^2/4)) - 25), so |xw| <= 2^25;                 */
+/*  3. R[lag] = sum_i xw(i) xw(i-lag) exactly in i64 (order-free);          */
+/*  4. Levinson-Durbin in IEEE double, the operation order below, no FMA;  */
+/*  5. quantisation to 15-bit coefficients: shift = 14 - e where           */
+/*     max|a| = f 2^e, f in [0.5,1); shift > 15 -> 15; shift < 0 -> order  */
+/*     unusable; round half away from zero with error feedback;            */
+/*  6. residual e(i) = x(i) - ((sum_t c_t x(i-1-t)) >> shift) in i64; an   */
+/*     order with a coded residual outside [-2^30, 2^30) is unusable (its  */
+/*     zigzag code then fits 31 bits, so an escape is always possible);    */
+/*  7. every order 1..Q (Q < n) gets the fixed path's Rice search with q   */
+/*     warm-ups; subframe total = rice + q (bps' + 15) + 9; the lowest      */
+/*     order with the strictly smallest total wins, and it replaces the     */
+/*     fixed/verbatim choice only if strictly smaller (totals incl. warm-ups)*/
+/* ===================================================================== */
+#define LPC_XW_BITS 25u
+
+int oracle_lpc_autocorr(const int64_t *x, uint32_t n, unsigned max_lag, int64_t *R) {
+    uint64_t m = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint64_t a = (uint64_t)(x[i] < 0 ? -x[i] : x[i]);
+        if (a > m) m = a;
+    }
+    uint64_t wmax = ((uint64_t)(n + 1) * (uint64_t)(n + 1)) / 4u;
+    int sh = (int)bitlen64(m) + (int)bitlen64(wmax) - (int)LPC_XW_BITS;
+    if (sh < 0) sh = 0;
+    int64_t *xw = (int64_t *)malloc((n ? n : 1) * sizeof(int64_t));
+    for (uint32_t i = 0; i < n; i++) {
+        int64_t w = (int64_t)(i + 1) * (int64_t)(n - i);
+        xw[i] = (x[i] * w) >> sh;
+    }
+    for (unsigned lag = 0; lag <= max_lag; lag++) {
+        int64_t acc = 0;
+        for (uint32_t i = lag; i < n; i++) acc += xw[i] * xw[i - lag];
+        R[lag] = acc;
+    }
+    free(xw);
+    return sh;
+}
+
+int oracle_lpc_levinson(const int64_t *R, unsigned max_order, double *coefs) {
+    double r[ORACLE_LPC_MAX_ORDER + 1], a[ORACLE_LPC_MAX_ORDER], tmp[ORACLE_LPC_MAX_ORDER];
+    for (unsigned i = 0; i <= max_order; i++) r[i] = (double)R[i];
+    if (!(r[0] > 0.0)) return 0;
+    double err = r[0];
+    unsigned valid = 0;
+    for (unsigned m = 0; m < max_order; m++) {
+        double acc = r[m + 1];
+        for (unsigned t = 0; t < m; t++) {
+            double p = a[t] * r[m - t];
+            acc = acc - p;
+        }
+        double k = acc / err;
+        for (unsigned t = 0; t < m; t++) {
+            double p = k * a[m - 1 - t];
+            tmp[t] = a[t] - p;
+        }
+        for (unsigned t = 0; t < m; t++) a[t] = tmp[t];
+        a[m] = k;
+        for (unsigned t = 0; t <= m; t++) coefs[m * ORACLE_LPC_MAX_ORDER + t] = a[t];
+        valid = m + 1;
+        double kk = k * k;
+        err = err * (1.0 - kk);
+        if (!(err > 0.0)) break;
+    }
+    return (int)valid;
+}
+
+int oracle_lpc_quantize(const double *a, unsigned order, unsigned precision, int32_t *q, int *shift) {
+    double cmax = 0.0;
+    for (unsigned t = 0; t < order; t++) {
+        double v = a[t] < 0.0 ? -a[t] : a[t];
+        if (v > cmax) cmax = v;
+    }
+    if (!(cmax > 0.0)) return -1;
+    int e;
+    frexp(cmax, &e);
+    int sh = (int)precision - 1 - e;
+    if (sh > 15) sh = 15;
+    if (sh < 0) return -1;
+    const double scale = (double)(1u << sh);
+    const int64_t qmax = ((int64_t)1 << (precision - 1)) - 1, qmin = -((int64_t)1 << (precision - 1));
+    double carry = 0.0;
+    for (unsigned t = 0; t < order; t++) {
+        double v = a[t] * scale;
+        v = v + carry;
+        int64_t qi = v >= 0.0 ? (int64_t)floor(v + 0.5) : -(int64_t)floor(-v + 0.5);
+        if (qi > qmax) qi = qmax;
+        if (qi < qmin) qi = qmin;
+        carry = v - (double)qi;
+        q[t] = (int32_t)qi;
+    }
+    *shift = sh;
+    return 0;
+}
+
+/* residuals of one quantised predictor; returns -1 if any leaves [-2^30, 2^30) */
+static int lpc_residuals(const int64_t *s, uint32_t n, unsigned order, const int32_t *c, int shift, int32_t *e) {
+    for (uint32_t i = 0; i < order && i < n; i++) e[i] = 0;
+    for (uint32_t i = order; i < n; i++) {
+        int64_t acc = 0;
+        for (unsigned t = 0; t < order; t++) acc += (int64_t)c[t] * s[i - 1 - t];
+        int64_t v = s[i] - (acc >> shift);
+        if (v < -(INT64_C(1) << 30) || v >= (INT64_C(1) << 30)) return -1;
+        e[i] = (int32_t)v;
+    }
+    return 0;
+}
+
+/* ===================================================================== */
 /* Encoder decisions (encoder.zig)                                         */
 /* ===================================================================== */
 typedef struct {
@@ -405,6 +521,47 @@ static unsigned calc_waste(int64_t *s, uint32_t n, unsigned bps) {
         for (uint32_t i = 0; i < n; i++) s[i] = (int64_t)(int32_t)(s[i] >> w); /* @intCast into i32 plane */
     return w;
 }
+
+/* LPC order search (build-defined, contract above).  Replaces the current
+ * choice when an order's total is strictly smaller. */
+static void lpc_search(sub_t *sub, const int64_t *s, uint32_t n, const oracle_config *cfg, unsigned bps,
+                       unsigned Q) {
+    oracle_subframe *r = &sub->rec;
+    int64_t R[ORACLE_LPC_MAX_ORDER + 1];
+    static __thread double coefs[ORACLE_LPC_MAX_ORDER * ORACLE_LPC_MAX_ORDER];
+    oracle_lpc_autocorr(s, n, Q, R);
+    int valid = oracle_lpc_levinson(R, Q, coefs);
+    int32_t *e = (int32_t *)malloc(n * sizeof(int32_t));
+    for (unsigned q = 1; q <= (unsigned)valid; q++) {
+        int32_t c[ORACLE_LPC_MAX_ORDER];
+        int shift;
+        if (oracle_lpc_quantize(coefs + (q - 1) * ORACLE_LPC_MAX_ORDER, q, ORACLE_LPC_PRECISION, c, &shift)) continue;
+        if (lpc_residuals(s, n, q, c, shift, e)) continue;
+        rice_cfg rc;
+        memset(&rc, 0, sizeof(rc));
+        int clamped = 0;
+        uint64_t rice = rice_params(e, n, cfg->max_rice_part_order, cfg->max_rice_param, bps, q, &rc, &clamped);
+        uint64_t total = rice + (uint64_t)q * (bps + ORACLE_LPC_PRECISION) + 9u;
+        if (total < r->estimate) {
+            r->type = OR_LPC;
+            r->estimate = total;
+            r->order = (uint8_t)q;
+            r->part_order = rc.part_order;
+            r->method = rc.method;
+            r->ub_clamped = (uint8_t)clamped;
+            memcpy(r->params, rc.params, sizeof(rc.params));
+            r->lpc_precision = ORACLE_LPC_PRECISION;
+            r->lpc_shift = (int8_t)shift;
+            memset(r->lpc_coefs, 0, sizeof(r->lpc_coefs));
+            memcpy(r->lpc_coefs, c, q * sizeof(int32_t));
+            memcpy(sub->residuals, e, n * sizeof(int32_t));
+        }
+    }
+    free(e);
+}
+
+static void choose_fixed(sub_t *sub, const int64_t *s, uint32_t n, int32_t *res, const oracle_config *cfg,
+                         unsigned bps, int i64_samples);
 
 /* chooseSubframeEncoding (encoder.zig:482-554).  `i64_samples` marks the
  * SampleVariant.wide side channel (32-bit stereo, waste 0). */
@@ -424,7 +581,17 @@ static void choose_subframe(sub_t *sub, int64_t *s, uint32_t n, int32_t *res, co
     if (all_eq) { r->type = OR_CONSTANT; r->estimate = bps; r->constant = s[0]; return; }
     r->type = OR_VERBATIM;
     r->estimate = (uint64_t)n * bps;
-    if (n <= 4) return;
+    const unsigned lpc_q = cfg->prediction;
+    if (n > 4) choose_fixed(sub, s, n, res, cfg, bps, i64_samples);
+    /* LPC mode (build-defined extension) */
+    if (lpc_q && n > lpc_q && n <= 4096) lpc_search(sub, s, n, cfg, bps, lpc_q);
+}
+
+/* The fixed-predictor part of chooseSubframeEncoding (encoder.zig:514-550). */
+static void choose_fixed(sub_t *sub, const int64_t *s, uint32_t n, int32_t *res, const oracle_config *cfg,
+                         unsigned bps, int i64_samples) {
+    oracle_subframe *r = &sub->rec;
+    const unsigned lpc_q = cfg->prediction;
     int wide = !(bps < 28 && !i64_samples);
     r->wide = (uint8_t)wide;
     int k = oracle_best_order(s, n, wide, NULL);
@@ -435,6 +602,8 @@ static void choose_subframe(sub_t *sub, int64_t *s, uint32_t n, int32_t *res, co
     int clamped = 0;
     uint64_t fixed_size = rice_params(res, n, cfg->max_rice_part_order, cfg->max_rice_param, bps, (unsigned)k,
                                       &rc, &clamped);
+    /* LPC mode (build-defined): estimates are whole payloads, warm-ups included */
+    if (lpc_q) fixed_size += (uint64_t)k * bps;
     if (fixed_size < r->estimate) { /* strict (encoder.zig:538) */
         r->type = OR_FIXED;
         r->estimate = fixed_size;
@@ -547,13 +716,21 @@ static void write_subframe(bw_t *w, const sub_t *sub, uint32_t n) {
         for (uint32_t i = 0; i < n; i++) bw_bits_signed(w, bps, (uint64_t)sub->samples[i]);
         return;
     }
-    /* FIXED (frame_writer.zig:303-361) */
+    /* FIXED (frame_writer.zig:303-361); LPC (build-defined, FLAC subframe syntax:
+     * type 0b1xxxxx = order-1, warm-ups, 4-bit precision-1, 5-bit signed shift,
+     * coefficients, then the same residual coding) */
     unsigned order = r->order, method = r->method;
     unsigned param_len = 4 + method;
     uint32_t pc = 1u << r->part_order;
-    if (waste == 0) bw_bits(w, 8, (8 | order) << 1);
-    else { bw_bits(w, 8, ((8 | order) << 1) | 1); bw_bits(w, waste, 1); }
+    unsigned tcode = r->type == OR_LPC ? (0x20u | (order - 1u)) : (8u | order);
+    if (waste == 0) bw_bits(w, 8, tcode << 1);
+    else { bw_bits(w, 8, (tcode << 1) | 1); bw_bits(w, waste, 1); }
     for (unsigned i = 0; i < order; i++) bw_bits_signed(w, bps, (uint64_t)sub->samples[i]);
+    if (r->type == OR_LPC) {
+        bw_bits(w, 4, r->lpc_precision - 1u);
+        bw_bits_signed(w, 5, (uint64_t)(int64_t)r->lpc_shift);
+        for (unsigned i = 0; i < order; i++) bw_bits_signed(w, r->lpc_precision, (uint64_t)(int64_t)r->lpc_coefs[i]);
+    }
     bw_bits(w, 6, (method << 4) | r->part_order);
     const int32_t *rem = sub->residuals + order;
     uint32_t part_len = (n >> r->part_order) - order;

@@ -38,10 +38,15 @@ typedef struct {
     uint8_t stereo_decorrelation; /* default true */
     uint8_t max_rice_part_order;  /* default 8 */
     uint8_t max_rice_param;       /* default 30 (rice.MAX_PARAM) */
-    uint8_t prediction;           /* unused by the reference (encoder.zig:629-640) */
+    uint8_t prediction;           /* unused by the reference (encoder.zig:629-640).  Build-defined
+                                     extension: 0 = fixed prediction only (the reference's output,
+                                     bit for bit); 1..32 = also search LPC orders 1..prediction
+                                     (see the LPC contract in flac_oracle.c / DESIGN.md) */
 } oracle_config;
 
-enum { OR_CONSTANT = 0, OR_VERBATIM = 1, OR_FIXED = 2 };
+enum { OR_CONSTANT = 0, OR_VERBATIM = 1, OR_FIXED = 2, OR_LPC = 3 };
+#define ORACLE_LPC_MAX_ORDER 32
+#define ORACLE_LPC_PRECISION 15   /* quantised coefficient bits (FLAC field max) */
 
 /* Decision record of one evaluated subframe (SubframeType.Encoding,
  * encoder.zig:678-702, plus the estimate returned by chooseSubframeEncoding). */
@@ -57,6 +62,11 @@ typedef struct {
     uint64_t estimate;   /* bit estimate used for decisions */
     int64_t constant;    /* CONSTANT value (shifted), 0 when undefined (bps'==0) */
     uint8_t params[256]; /* rice Param.p for the chosen order: p, or 0x80|bits */
+    /* LPC only (build-defined extension) */
+    uint8_t lpc_precision;
+    int8_t lpc_shift;
+    uint8_t pad2[6];
+    int32_t lpc_coefs[ORACLE_LPC_MAX_ORDER];
 } oracle_subframe;
 
 typedef struct {
@@ -127,6 +137,15 @@ void oracle_streaminfo_bytes(const oracle_streaminfo *si, uint8_t out[34]);
 
 /* maxFrameBytes (encoder.zig:583-595). */
 size_t oracle_max_frame_bytes(uint32_t block_size, uint32_t bit_depth, uint32_t channels);
+
+/* LPC pieces (build-defined; exposed for unit tests).  x: n shifted samples.
+ * autocorr: R[0..max_lag] exact (returns the scaling shift sh).
+ * levinson: coefs[(q-1)*32 + t] for orders q = 1..max_order; returns the
+ * number of orders with valid coefficients.
+ * quantize: returns 0 and the shift, or -1 if the order is not representable. */
+int oracle_lpc_autocorr(const int64_t *x, uint32_t n, unsigned max_lag, int64_t *R);
+int oracle_lpc_levinson(const int64_t *R, unsigned max_order, double *coefs);
+int oracle_lpc_quantize(const double *a, unsigned order, unsigned precision, int32_t *q, int *shift);
 
 /* Exposed pieces for unit tests. */
 uint64_t oracle_rice_part_size(uint64_t len, uint32_t param, uint64_t abs_sum);

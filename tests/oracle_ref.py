@@ -22,7 +22,9 @@ class OSub(ctypes.Structure):
     _fields_ = [("type", ctypes.c_uint8), ("waste", ctypes.c_uint8), ("bits", ctypes.c_uint8),
                 ("order", ctypes.c_uint8), ("part_order", ctypes.c_uint8), ("method", ctypes.c_uint8),
                 ("wide", ctypes.c_uint8), ("ub_clamped", ctypes.c_uint8), ("estimate", ctypes.c_uint64),
-                ("constant", ctypes.c_int64), ("params", ctypes.c_uint8 * 256)]
+                ("constant", ctypes.c_int64), ("params", ctypes.c_uint8 * 256),
+                ("lpc_precision", ctypes.c_uint8), ("lpc_shift", ctypes.c_int8), ("pad2", ctypes.c_uint8 * 6),
+                ("lpc_coefs", ctypes.c_int32 * 32)]
 
 
 class ORec(ctypes.Structure):
@@ -57,8 +59,8 @@ def lib():
     return _L
 
 
-def config(channels, bits, rate, block=4096, stereo=True, part_order=8, param=30):
-    return OConfig(rate, block, channels, bits, 1 if stereo else 0, part_order, param, 0)
+def config(channels, bits, rate, block=4096, stereo=True, part_order=8, param=30, lpc=0):
+    return OConfig(rate, block, channels, bits, 1 if stereo else 0, part_order, param, lpc)
 
 
 def encode_stream(pcm: bytes, channels: int, bits: int, rate: int, block: int = 4096, first_frame: int = 0,
@@ -97,11 +99,11 @@ def encode_frame(planes, n: int, frame_number: int, channels: int, bits: int, ra
     return out.raw[:r], rec
 
 
-def encode_file(pcm: bytes, channels: int, bits: int, rate: int, block: int = 4096):
+def encode_file(pcm: bytes, channels: int, bits: int, rate: int, block: int = 4096, **kw):
     L = lib()
     B = bits // 8
     n = len(pcm) // (channels * B)
-    cfg = config(channels, bits, rate, block)
+    cfg = config(channels, bits, rate, block, **kw)
     nf = (n + block - 1) // block
     cap = 200 + nf * L.oracle_max_frame_bytes(block, bits, channels)
     out = ctypes.create_string_buffer(cap)

@@ -57,6 +57,8 @@ def check_stream(ch, bits, rate, n, stream=0, first_frame=0, specials=True, deco
         okw["part_order"] = kw["max_rice_part_order"]
     if "max_rice_param" in kw:
         okw["param"] = kw["max_rice_param"]
+    if "lpc_order" in kw:
+        okw["lpc"] = kw["lpc_order"]
     block = kw.get("block_size", 4096)
     ref, ref_sizes, ref_md5 = oracle_ref.encode_stream(pcm, ch, bits, rate, block=block, first_frame=first_frame,
                                                        **okw)
@@ -115,9 +117,9 @@ def test_block_size_1152():
     check_stream(2, 16, 44100, 1152 * 40 + 5, block_size=1152)
 
 
-def _records_match(ch, bits, rate, n, stream=0):
+def _records_match(ch, bits, rate, n, stream=0, lpc=0):
     pcm = synth.synth_pcm(n, ch, bits, rate, stream=stream)
-    enc = gpu_encoder(ch, bits, rate)
+    enc = gpu_encoder(ch, bits, rate, **({"lpc_order": lpc} if lpc else {}))
     enc.set_records(True)
     try:
         got, sizes = enc.encode_frames(pcm)
@@ -130,17 +132,20 @@ def _records_match(ch, bits, rate, n, stream=0):
     for f, rec in enumerate(recs):
         planes = [np.ascontiguousarray(samples[f * bs:(f + 1) * bs, c]).astype(np.int32) for c in range(ch)]
         nn = len(planes[0])
-        ref_bytes, orec = oracle_ref.encode_frame(planes, nn, f, ch, bits, rate)
+        ref_bytes, orec = oracle_ref.encode_frame(planes, nn, f, ch, bits, rate, lpc=lpc)
         assert rec.channel_code == orec.channel_code, f"frame {f} channel code"
         for c in range(orec.n_cand):
             g, o = rec.cand[c], orec.cand[c]
             ctx = f"frame {f} cand {c}"
             assert (g.type, g.waste, g.bits) == (o.type, o.waste, o.bits), ctx
             assert g.estimate == o.estimate, ctx + f" estimate {g.estimate} vs {o.estimate}"
-            if o.type == 2:
+            if o.type >= 2:
                 assert (g.order, g.part_order, g.method) == (o.order, o.part_order, o.method), ctx
                 np_ = 1 << o.part_order
                 assert list(g.params)[:np_] == list(o.params)[:np_], ctx
+            if o.type == 3:
+                assert (g.lpc_precision, g.lpc_shift) == (o.lpc_precision, o.lpc_shift), ctx
+                assert list(g.lpc_coefs)[:o.order] == list(o.lpc_coefs)[:o.order], ctx
             if o.type == 0:
                 assert g.constant == o.constant, ctx
     return got

@@ -173,7 +173,9 @@ int validate(const flacgpu_config *cfg) {
     if (cfg->max_rice_part_order > kMaxPartOrder) return FLACGPU_ERR_INVALID_CONFIG;  // rice.zig:13 buffers
     if (cfg->max_rice_param < 1 || cfg->max_rice_param > 30) return FLACGPU_ERR_INVALID_CONFIG;
     if (cfg->sample_rate >= (1u << 20)) return FLACGPU_ERR_INVALID_CONFIG;  // u20 (wav_reader.zig:98)
-    if (cfg->prediction != 0) return FLACGPU_ERR_INVALID_CONFIG;  // only fixed prediction exists
+    // prediction: 0 = fixed only (the reference); 1..12 = LPC search up to that order
+    // (build-defined extension; the FLAC subset limit)
+    if (cfg->prediction > kLpcMax) return FLACGPU_ERR_INVALID_CONFIG;
     return FLACGPU_OK;
 }
 
@@ -200,6 +202,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.stereo = c->stereo;
     a.max_part_order = c->cfg.max_rice_part_order;
     a.max_param = c->cfg.max_rice_param;
+    a.lpc_order = c->cfg.prediction;
     a.block_size = c->cfg.block_size;
     a.desc = d_desc;
     a.desc_stride = c->desc_stride;
@@ -346,9 +349,10 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     c->nt_pack = 64u * n_out;
     c->image_bytes = fg_round16(frame_bound_bytes(kBlock, c->C, c->bits, c->stereo != 0) + 16u);
     c->desc_stride = desc_stride(n_out);
-    c->stage_dbuf = ana_layout(c->C, c->B, nw, true, true).total <= 160u * 1024u;
-    c->lds = ana_layout(c->C, c->B, nw, true, c->stage_dbuf).total;
-    c->lds_tail = ana_layout(c->C, c->B, nw, false, false).total;
+    const bool lpc = c->cfg.prediction != 0;
+    c->stage_dbuf = ana_layout(c->C, c->B, nw, true, true, lpc).total <= 160u * 1024u;
+    c->lds = ana_layout(c->C, c->B, nw, true, c->stage_dbuf, lpc).total;
+    c->lds_tail = ana_layout(c->C, c->B, nw, false, false, lpc).total;
     c->lds_pack = pack_layout(c->C, c->B, c->image_bytes).total;
     // CRC fold: half-segments of H words (odd), H <= ceil(image words / (2 * pack threads))
     c->crc_hmax = ((c->image_bytes / 4u + 2u * c->nt_pack - 1u) / (2u * c->nt_pack)) | 1u;

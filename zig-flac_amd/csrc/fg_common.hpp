@@ -11,6 +11,11 @@ constexpr int kLaneSamples = 64;   // samples per lane: one wave == one 4096-sam
 constexpr int kMaxPartOrder = 8;   // rice.MAX_ORDER (rice.zig:13)
 constexpr int kParamBytes = 512;   // params of all orders 0..8: offset (1<<o)-1 (511 used)
 constexpr int kCrcThreadsMax = 512;
+// LPC (build-defined extension; the reference has none, readme.md:27): orders
+// 1..12 on the GPU path (the FLAC subset limit), 15-bit coefficients.
+constexpr int kLpcMax = 12;
+constexpr int kLpcPrec = 15;
+constexpr int kLpcTab = 160;       // i32 per wave: [12 orders][13] (12 coefs + shift)
 
 // One frame of work.  pcm_off must be 4-byte aligned.
 struct FrameJob {
@@ -23,7 +28,7 @@ struct FrameJob {
 // Per-candidate decision record (SubframeType.Encoding + estimate,
 // encoder.zig:678-702).  Mirrors flacgpu_subframe_record.
 struct SubRec {
-    uint8_t type;       // 0 CONSTANT, 1 VERBATIM, 2 FIXED
+    uint8_t type;       // 0 CONSTANT, 1 VERBATIM, 2 FIXED, 3 LPC
     uint8_t waste;
     uint8_t bits;
     uint8_t order;
@@ -35,6 +40,10 @@ struct SubRec {
     uint64_t estimate;
     int64_t constant;
     uint8_t params[256];
+    uint8_t lpc_precision;
+    int8_t lpc_shift;
+    uint8_t pad3[6];
+    int32_t lpc_coefs[32];
 };
 
 struct FrameRec {
@@ -49,22 +58,23 @@ struct FrameRec {
 // kernel: everything needed to emit the frame's bits at its final byte offset
 // without redoing the search.  Stride: desc_stride(n_out).
 struct SubDesc {
-    uint8_t type;        // 0 CONSTANT, 1 VERBATIM, 2 FIXED
+    uint8_t type;        // 0 CONSTANT, 1 VERBATIM, 2 FIXED, 3 LPC
     uint8_t waste;
     uint8_t bd;          // bits of the (side: +1) channel before the waste shift
-    uint8_t order;       // fixed predictor order
+    uint8_t order;       // fixed / LPC predictor order (= warm-up samples)
     uint8_t porder;      // rice partition order
     uint8_t method;      // 0 RICE, 1 RICE2
     uint8_t cand;        // stereo: 0 L, 1 R, 2 M, 3 S; else the channel
-    uint8_t pad;
+    int8_t lpc_shift;    // LPC: quantisation shift
     uint32_t bits;       // exact subframe bits
-    uint32_t pad2;
+    uint32_t lpc_prec;   // LPC: coefficient precision
     int64_t cval;        // CONSTANT value (after the waste shift)
     uint32_t lane_bits[64];  // bits of lane l's 64-sample segment (pass A)
     uint8_t params[256];     // rice params of the chosen order (0x80|w = escape)
+    int16_t coef[kLpcMax];   // LPC: quantised coefficients
     uint8_t pad3[8];
 };
-static_assert(sizeof(SubDesc) == 544, "SubDesc layout");
+static_assert(sizeof(SubDesc) == 568, "SubDesc layout");
 
 struct FrameDesc {
     uint32_t hdr_bytes;     // frame header bytes incl. CRC-8
@@ -75,7 +85,7 @@ struct FrameDesc {
 };
 static_assert(sizeof(FrameDesc) == 32, "FrameDesc layout");
 
-__host__ __device__ constexpr uint32_t desc_stride(uint32_t n_out) { return 32u + n_out * 544u; }
+__host__ __device__ constexpr uint32_t desc_stride(uint32_t n_out) { return 32u + n_out * (uint32_t)sizeof(SubDesc); }
 
 struct EncodeArgs {
     const uint8_t *pcm;         // device PCM base
@@ -89,6 +99,7 @@ struct EncodeArgs {
     uint32_t max_part_order;    // 0..8
     uint32_t max_param;         // 1..30
     uint32_t block_size;        // stream block size (header field for short frames is n)
+    uint32_t lpc_order;         // 0: fixed prediction only (the reference); 1..12: LPC search
     uint8_t *desc;              // frame descriptors [slot], desc_stride bytes each
     uint32_t desc_stride;
     uint32_t image_bytes;       // pack kernel LDS frame-image bytes (multiple of 16, >= bound + 16)

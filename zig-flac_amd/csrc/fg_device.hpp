@@ -369,6 +369,7 @@ __device__ __forceinline__ int32_t ld_sample(const uint8_t *p) {
 
 struct CandRes {
     uint32_t type, waste, bd, order, porder, method;
+    int32_t lsh;  // LPC quantisation shift
     uint64_t est;
     int64_t cval;
 };
@@ -575,6 +576,172 @@ __device__ __forceinline__ void residuals_generic(ST (&s)[64], ST h1, ST h2, ST 
 }
 
 // ------------------------------------------------------------------------
+// LPC (build-defined extension: the reference has no LPC, readme.md:27,
+// encoder.zig:629-640,694-699).  The contract is stated once in
+// oracle/flac_oracle.c ("LPC -- build-defined extension") and followed here
+// operation for operation: integer Welch window (i+1)(n-i), windowed samples
+// scaled to <= 25 bits, exact i64 autocorrelation, Levinson-Durbin in IEEE
+// double in a fixed order (the library is built with -ffp-contract=off),
+// 15-bit coefficients with error feedback, residuals in i64.
+// ------------------------------------------------------------------------
+
+// R[0..W] of the lane-distributed samples s (lane l owns [64l, 64l+64); zero past n).
+template <int W, typename ST>
+__device__ __forceinline__ void lpc_autocorr(const ST (&s)[64], uint32_t n, uint32_t l, int64_t (&R)[W + 1]) {
+    uint64_t ov = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const int64_t x = (int64_t)s[j];
+        ov |= (uint64_t)(x < 0 ? -x : x);
+    }
+    const uint32_t mb = bitlen64(wave_or64(ov));
+    const uint32_t wb = bitlen32(((n + 1u) * (n + 1u)) >> 2);
+    const int32_t shv = (int32_t)(mb + wb) - 25;
+    const uint32_t sh = shv > 0 ? (uint32_t)shv : 0u;
+    auto xw = [&](int j) -> int32_t {
+        const uint32_t i = l * 64u + (uint32_t)j;
+        const int32_t w = i < n ? (int32_t)((i + 1u) * (n - i)) : 0;
+        int64_t p;
+        if constexpr (sizeof(ST) == 4) p = (int64_t)(int32_t)s[j] * (int64_t)w;
+        else p = (int64_t)s[j] * (int64_t)w;
+        return (int32_t)(p >> sh);
+    };
+    int32_t hx[W];
+#pragma unroll
+    for (int t = 0; t < W; t++) hx[t] = shr1(xw(63 - t));  // the previous lane's last W
+    int64_t acc[W + 1];
+#pragma unroll
+    for (int g = 0; g <= W; g++) acc[g] = 0;
+    int32_t xv[64];
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        xv[j] = xw(j);
+#pragma unroll
+        for (int g = 0; g <= W; g++) {
+            const int32_t y = (j - g >= 0) ? xv[(j - g) >= 0 ? (j - g) : 0] : hx[(g - j - 1) >= 0 ? (g - j - 1) : 0];
+            acc[g] += (int64_t)xv[j] * (int64_t)y;
+        }
+    }
+#pragma unroll
+    for (int g = 0; g <= W; g++) R[g] = (int64_t)wave_sum64((uint64_t)acc[g]);
+}
+
+// Levinson-Durbin + quantisation of every order 1..Q (all lanes compute the same
+// values; lane `writer` stores them): tab[(q-1)*13 + t] = coefficient t of order q
+// (0 past q), tab[(q-1)*13 + 12] = its shift, or -1 if the order is unusable.
+template <int W>
+__device__ __forceinline__ void lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q, int32_t *tab, bool writer) {
+#pragma clang fp contract(off)
+    if (writer)
+        for (uint32_t q = 0; q < (uint32_t)kLpcMax; q++) tab[q * 13u + 12u] = -1;
+    double r[W + 1], a[W], tmp[W];
+#pragma unroll
+    for (int i = 0; i <= W; i++) r[i] = (double)R[i];
+    if (!(r[0] > 0.0)) return;
+    double err = r[0];
+    bool live = true;  // uniform: order m+1 is computed while live (stops at Q or when err <= 0)
+#pragma unroll
+    for (int m = 0; m < W; m++) {
+        live = live && (uint32_t)m < Q;
+        if (!live) continue;
+        double acc = r[m + 1];
+#pragma unroll
+        for (int t = 0; t < m; t++) {
+            const double p = a[t] * r[m - t];
+            acc = acc - p;
+        }
+        const double k = acc / err;
+#pragma unroll
+        for (int t = 0; t < m; t++) {
+            const double p = k * a[m - 1 - t];
+            tmp[t] = a[t] - p;
+        }
+#pragma unroll
+        for (int t = 0; t < m; t++) a[t] = tmp[t];
+        a[m] = k;
+        // quantise order m+1 (oracle_lpc_quantize)
+        double cmax = 0.0;
+#pragma unroll
+        for (int t = 0; t <= m; t++) {
+            const double v = a[t] < 0.0 ? -a[t] : a[t];
+            cmax = v > cmax ? v : cmax;
+        }
+        int32_t shq = -1;
+        int32_t qc[W];
+#pragma unroll
+        for (int t = 0; t < W; t++) qc[t] = 0;
+        if (cmax > 0.0) {
+            int e;
+            (void)frexp(cmax, &e);
+            shq = kLpcPrec - 1 - e;
+            if (shq > 15) shq = 15;
+            if (shq >= 0) {
+                const double scale = (double)(1u << shq);
+                const int64_t qmax = (1ll << (kLpcPrec - 1)) - 1, qmin = -(1ll << (kLpcPrec - 1));
+                double carry = 0.0;
+#pragma unroll
+                for (int t = 0; t <= m; t++) {
+                    double v = a[t] * scale;
+                    v = v + carry;
+                    int64_t qi = v >= 0.0 ? (int64_t)floor(v + 0.5) : -(int64_t)floor(-v + 0.5);
+                    qi = qi > qmax ? qmax : (qi < qmin ? qmin : qi);
+                    carry = v - (double)qi;
+                    qc[t] = (int32_t)qi;
+                }
+            }
+        }
+        if (writer) {
+#pragma unroll
+            for (int t = 0; t < kLpcMax; t++) tab[m * 13 + t] = (t < W) ? qc[t < W ? t : 0] : 0;
+            tab[m * 13 + 12] = shq;
+        }
+        const double kk = k * k;
+        err = err * (1.0 - kk);
+        live = err > 0.0;
+    }
+}
+
+// Prediction sum_t c[t] * x[j-1-t] over the lane's samples and the previous lane's
+// last W samples hs[] (hs[t] = sample 64l-1-t); c[t] = 0 past the order.
+template <int W, typename ST>
+__device__ __forceinline__ int64_t lpc_pred(const ST (&s)[64], const ST (&hs)[W], const int32_t (&c)[W], int j) {
+    int64_t acc = 0;
+#pragma unroll
+    for (int t = 0; t < W; t++) {
+        const int idx = j - 1 - t;
+        const ST x = idx >= 0 ? s[idx >= 0 ? idx : 0] : hs[(-idx - 1) >= 0 ? (-idx - 1) : 0];
+        if constexpr (sizeof(ST) == 4) acc += (int64_t)c[t] * (int64_t)(int32_t)x;
+        else acc += (int64_t)c[t] * (int64_t)x;
+    }
+    return acc;
+}
+
+// LPC residuals read-only over s: f(j, warm, e) with e the exact i64 residual.
+template <int W, typename ST, typename F>
+__device__ __forceinline__ void residuals_lpc(const ST (&s)[64], const ST (&hs)[W], const int32_t (&c)[W],
+                                              uint32_t shift, uint32_t q, uint32_t l, F &&f) {
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const int64_t e = (int64_t)s[j] - (lpc_pred<W, ST>(s, hs, c, j) >> shift);
+        const bool warm = (j < W) && (l == 0) && ((uint32_t)j < q);
+        f(j, warm, e);
+    }
+}
+
+// LPC residuals in place (descending, so every prediction reads original samples);
+// lane 0 keeps its q warm-up samples.
+template <int W, typename ST>
+__device__ __forceinline__ void residuals_lpc_inplace(ST (&s)[64], const ST (&hs)[W], const int32_t (&c)[W],
+                                                      uint32_t shift, uint32_t q, uint32_t l) {
+#pragma unroll
+    for (int j = 63; j >= 0; j--) {
+        const int64_t e = (int64_t)s[j] - (lpc_pred<W, ST>(s, hs, c, j) >> shift);
+        const bool warm = (j < W) && (l == 0) && ((uint32_t)j < q);
+        if (!warm) s[j] = (ST)(int32_t)e;
+    }
+}
+
+// ------------------------------------------------------------------------
 // Kernel 1: frame analysis.  One workgroup per frame (persistent loop), one
 // wave per candidate subframe.  Decides every candidate exactly as
 // Encoder.writeFrame does (encoder.zig:234-284, 482-570), measures the exact
@@ -594,12 +761,16 @@ __device__ __forceinline__ void residuals_generic(ST (&s)[64], ST h1, ST h2, ST 
 #ifndef FG_PACK_MINW
 #define FG_PACK_MINW 4
 #endif
-template <int B, int CLS, bool FULL, int MAXT, int NC>
-// i64 samples (32-bit input) and the tail kernels' LDS tables need the larger
-// register budget (2 waves/SIMD); the rest fits 128 VGPRs (4 waves/SIMD).
-__global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG_MINW : 2)) k_analyze(EncodeArgs a) {
+template <int B, int CLS, bool FULL, int MAXT, int NC, int LPW>
+// i64 samples (32-bit input), the tail kernels' LDS tables and the LPC search need
+// the larger register budget (2 waves/SIMD); the rest fits 128 VGPRs (4 waves/SIMD).
+//   LPW  : 0 = fixed prediction only (the reference); 8 / 12 = LPC taps held in
+//          registers (orders up to LPW, build-defined extension)
+__global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LPW == 0) ? FG_MINW : 2))
+    k_analyze(EncodeArgs a) {
     using ST = typename Cls<CLS>::S;
-    using SumT = typename Cls<CLS>::Sum;
+    // LPC residuals may reach 2^30 in magnitude: 16-sample sums need 64 bits
+    using SumT = typename std::conditional<LPW == 0, typename Cls<CLS>::Sum, uint64_t>::type;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
     const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
@@ -609,8 +780,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
     const uint32_t cw = 16u * C * B;           // dwords per 64-sample chunk
     const uint32_t cst = cw + stage_pad(C, B);  // LDS chunk stride (dwords)
     const bool dbuf = FULL && a.stage_dbuf != 0;
-    const AnaLayout LY = ana_layout(C, B, NW, FULL, dbuf);
-    uint8_t *par = smem + LY.par + wave * 512u;
+    const AnaLayout LY = ana_layout(C, B, NW, FULL, dbuf, LPW > 0);
+    uint8_t *par = smem + LY.par + wave * LY.par_stride;
     uint32_t *recs = (uint32_t *)(smem + LY.rec);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
     const bool stereo = a.stereo != 0;
@@ -655,6 +826,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
         CandRes R;
         R.bd = bd;
         R.order = R.porder = R.method = 0;
+        R.lsh = 0;
         R.cval = 0;
         {
             uint64_t o;
@@ -800,53 +972,58 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
         }
         STAMP(3);
 
-        if (try_fixed) {
-            // ---- 6. residuals in place and the finest-level partition sums (rice.zig:288-340)
-            SumT S8[4] = {0, 0, 0, 0};
-            uint32_t O8[4] = {0, 0, 0, 0};
-            uint64_t *psum = nullptr;
-            uint32_t *pmax = nullptr;
-            uint32_t P = a.max_part_order, ps = 0;
+        // ---- 6/7. finest-level partition sums (rice.zig:288-340) and the parameter search for
+        // every partition order (rice.zig:248-279,343-405) of one residual set with kw warm-up
+        // samples -- shared by the fixed predictor and (build-defined) the LPC orders.
+        const uint32_t capp = bps > 16 ? 30u : 14u;
+        const uint32_t maxp = capp < a.max_param ? capp : a.max_param;
+        uint64_t *psum = nullptr;
+        uint32_t *pmax = nullptr;
+        if constexpr (!FULL) {
+            psum = (uint64_t *)(smem + LY.psum) + wave * 512u;
+            pmax = (uint32_t *)(smem + LY.pmax) + wave * 512u;
+        }
+        // caps of rice.calcParams (rice.zig:97-103).  The while-clamp only changes the reference's
+        // result where it would slice res[kw..ps] with ps < kw (UB there).  Full frames: n = 4096
+        // and kw <= 12 leave the configured order.
+        auto part_cap = [&](uint32_t kw) -> uint32_t {
+            uint32_t P = a.max_part_order;
             if constexpr (!FULL) {
-                // caps of rice.calcParams (rice.zig:97-103).  The while-clamp only changes the
-                // reference's result where it would slice res[k..ps] with ps < k (UB there).
-                const uint32_t lim = k ? (31u - __builtin_clz(n)) - (31u - __builtin_clz(k)) : 15u;
+                const uint32_t lim = kw ? (31u - __builtin_clz(n)) - (31u - __builtin_clz(kw)) : 15u;
                 const uint32_t ctzn = (uint32_t)__builtin_ctz(n);
                 if (ctzn < P) P = ctzn;
                 if (lim < P) P = lim;
-                while (P > 0 && (n >> P) < k) P--;
-                ps = n >> P;
-                psum = (uint64_t *)(smem + LY.psum) + wave * 512u;
-                pmax = (uint32_t *)(smem + LY.pmax) + wave * 512u;
+                while (P > 0 && (n >> P) < kw) P--;
+            }
+            return P;
+        };
+        auto zero_parts = [&]() {
+            if constexpr (!FULL) {
                 for (uint32_t i = l; i < 512u; i += 64) {
                     psum[i] = 0;
                     pmax[i] = 0;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
-            {
-                auto acc = [&](int j, bool warm, ST r) {
-                    const uint32_t zz = zigzag32((int32_t)r);
-                    const uint32_t av = (zz >> 1) + (zz & 1u);  // |r|
-                    if constexpr (FULL) {
-                        S8[j >> 4] += warm ? 0u : av;
-                        O8[j >> 4] |= warm ? 0u : zz;
-                    } else {
-                        const uint32_t i = l * 64u + j;
-                        if (!warm && i < n) {
-                            const uint32_t pid = i / ps;
-                            atomicAdd((unsigned long long *)&psum[pid], (unsigned long long)av);
-                            atomicOr(&pmax[pid], zz);
-                        }
-                    }
-                };
-                FG_DISPATCH_K(k, (residuals_k<K, ST>(s, h1, h2, h3, h4, l, acc)))
+        };
+        // residual r at lane position j -> finest-level sums (full: 4 lane-owned partitions of 16)
+        auto part_acc = [&](SumT (&S8)[4], uint32_t (&O8)[4], uint32_t ps, int j, bool warm, int32_t r) {
+            const uint32_t zz = zigzag32(r);
+            const uint32_t av = (zz >> 1) + (zz & 1u);  // |r|
+            if constexpr (FULL) {
+                S8[j >> 4] += warm ? 0u : av;
+                O8[j >> 4] |= warm ? 0u : zz;
+            } else {
+                const uint32_t i = l * 64u + j;
+                if (!warm && i < n) {
+                    const uint32_t pid = i / ps;
+                    atomicAdd((unsigned long long *)&psum[pid], (unsigned long long)av);
+                    atomicOr(&pmax[pid], zz);
+                }
             }
-            STAMP(4);
-
-            // ---- 7. parameter search for every partition order (rice.zig:248-279,343-395)
-            const uint32_t capp = bps > 16 ? 30u : 14u;
-            const uint32_t maxp = capp < a.max_param ? capp : a.max_param;
+        };
+        auto rice_search = [&](const SumT (&S8)[4], const uint32_t (&O8)[4], uint32_t kw, uint32_t P, uint8_t *pb,
+                               uint32_t &best_o, uint32_t &best_m) -> uint64_t {
             uint64_t tots[9];
             uint32_t fives[9];
             if constexpr (FULL) {
@@ -887,36 +1064,36 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                                 else if (o == 7) { S = q ? S7b : S7a; W = q ? W7b : W7a; }
                                 else { S = S6; W = W6; }
                                 const uint32_t j = l * per + q;
-                                const uint32_t len = (4096u >> o) - (j == 0 ? k : 0u);
+                                const uint32_t len = (4096u >> o) - (j == 0 ? kw : 0u);
                                 const uint32_t p = rice_choose(S, len, W, maxp, &c);
                                 cost += c;
                                 five |= (p < 0x80u && p > 14u);
-                                par[(1u << o) - 1u + j] = (uint8_t)p;
+                                pb[(1u << o) - 1u + j] = (uint8_t)p;
                             }
                             tots[o] = wave_sum32(cost);
                         } else if (o >= 2) {
                             const int g = 6 - o;  // a partition spans 2^g lanes
                             const uint32_t j = l >> g;
                             const bool lead = (l & ((1u << g) - 1u)) == 0;
-                            const uint32_t len = (4096u >> o) - (j == 0 ? k : 0u);
+                            const uint32_t len = (4096u >> o) - (j == 0 ? kw : 0u);
                             const uint32_t p = rice_choose(Sl[g - 1], len, Wl[g - 1], maxp, &c);
                             if (lead) {
                                 cost = c;
                                 five = (p < 0x80u && p > 14u);
-                                par[(1u << o) - 1u + j] = (uint8_t)p;
+                                pb[(1u << o) - 1u + j] = (uint8_t)p;
                             }
                             tots[o] = wave_sum32(cost);
                         } else {
                             // uniform: order 1 = rows {0,1} and {2,3}; order 0 = all rows
-                            const uint32_t len0 = (4096u >> o) - k, len1 = 4096u >> o;
+                            const uint32_t len0 = (4096u >> o) - kw, len1 = 4096u >> o;
                             uint32_t c0, c1 = 0, p1 = 0;
                             const uint32_t p0 = (o == 1) ? rice_choose(r0 + r1, len0, max(m0, m1), maxp, &c0)
                                                          : rice_choose(r0 + r1 + r2 + r3, len0,
                                                                        max(max(m0, m1), max(m2, m3)), maxp, &c0);
                             if (o == 1) p1 = rice_choose(r2 + r3, len1, max(m2, m3), maxp, &c1);
                             if (l == 0) {
-                                par[(1u << o) - 1u] = (uint8_t)p0;
-                                if (o == 1) par[2] = (uint8_t)p1;
+                                pb[(1u << o) - 1u] = (uint8_t)p0;
+                                if (o == 1) pb[2] = (uint8_t)p1;
                             }
                             five = (p0 < 0x80u && p0 > 14u) || (o == 1 && p1 < 0x80u && p1 > 14u);
                             tots[o] = (uint64_t)c0 + c1;
@@ -935,12 +1112,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                         uint32_t cost = 0;
                         bool five = false;
                         for (uint32_t j = l; j < np; j += 64) {
-                            const uint32_t len = len_full - (j == 0 ? k : 0u);
+                            const uint32_t len = len_full - (j == 0 ? kw : 0u);
                             uint32_t c;
                             const uint32_t p = rice_choose(cs[j], len, bitlen32(cm[j]), maxp, &c);
                             cost += c;
                             five |= (p < 0x80u && p > 14u);
-                            par[np - 1u + j] = (uint8_t)p;
+                            pb[np - 1u + j] = (uint8_t)p;
                         }
                         tots[o] = wave_sum32(cost);
                         fives[o] = (maxp > 14u && __any(five)) ? 1u : 0u;
@@ -957,7 +1134,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                 }
             }
             uint64_t best = ~0ull;
-            uint32_t best_o = 0, best_m = 0;
+            best_o = 0;
+            best_m = 0;
 #pragma unroll
             for (int o = 0; o < 9; o++) {
                 const uint64_t tot = tots[o] + ((uint64_t)(4u + fives[o]) << o);
@@ -967,6 +1145,29 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                     best_m = fives[o];
                 }
             }
+            return best;
+        };
+
+        // LPC mode (build-defined): estimates are whole payloads, warm-ups included
+        const bool lpc_on = LPW > 0 && a.lpc_order != 0;
+        uint32_t cur = 0;  // parameter buffer holding the current choice (LPC: 2 per wave)
+        if (try_fixed) {
+            // ---- 6. residuals (read-only over s) and the finest-level partition sums
+            SumT S8[4] = {0, 0, 0, 0};
+            uint32_t O8[4] = {0, 0, 0, 0};
+            const uint32_t P = part_cap(k);
+            const uint32_t ps = n >> P;
+            zero_parts();
+            {
+                auto acc = [&](int j, bool warm, ST r) { part_acc(S8, O8, ps, j, warm, (int32_t)r); };
+                FG_DISPATCH_K(k, (residuals_k<K, ST>(s, h1, h2, h3, h4, l, acc)))
+            }
+            STAMP(4);
+
+            // ---- 7. parameter search
+            uint32_t best_o, best_m;
+            uint64_t best = rice_search(S8, O8, k, P, par, best_o, best_m);
+            if (lpc_on) best += (uint64_t)k * bps;
 
             // ---- 8. FIXED iff its estimate < the verbatim estimate (encoder.zig:538)
             if (best < R.est) {
@@ -975,6 +1176,58 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                 R.order = k;
                 R.porder = best_o;
                 R.method = best_m;
+            }
+        }
+        int32_t *ltab = nullptr;
+        if constexpr (LPW > 0) {
+            // ---- 8b. LPC order search (oracle/flac_oracle.c lpc_search): every order 1..Q with
+            // usable coefficients; total = rice + q (bps' + 15) + 9; strictly smaller replaces
+            ltab = (int32_t *)(smem + LY.lpc) + wave * (uint32_t)kLpcTab;
+            const uint32_t Q = a.lpc_order;
+            if (lpc_on && R.type != 0 && n > Q) {
+                {
+                    int64_t Rac[LPW + 1];
+                    lpc_autocorr<LPW, ST>(s, n, l, Rac);
+                    lpc_coefs<LPW>(Rac, Q, ltab, l == 0);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                ST hs[LPW];
+#pragma unroll
+                for (int t = 0; t < LPW; t++) hs[t] = shr1(s[63 - t]);
+                for (uint32_t q = 1; q <= Q; q++) {
+                    const int32_t shq = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + 12u]);
+                    if (shq < 0) continue;
+                    int32_t c[LPW];
+#pragma unroll
+                    for (int t = 0; t < LPW; t++) c[t] = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + t]);
+                    SumT S8[4] = {0, 0, 0, 0};
+                    uint32_t O8[4] = {0, 0, 0, 0};
+                    const uint32_t P = part_cap(q);
+                    const uint32_t ps = n >> P;
+                    zero_parts();
+                    uint32_t bad = 0;
+                    auto acc = [&](int j, bool warm, int64_t e) {
+                        // usable only if every coded residual's zigzag fits 31 bits
+                        const bool valid = !warm && (FULL || l * 64u + (uint32_t)j < n);
+                        bad |= (valid && (uint64_t)(e + (1ll << 30)) >= (1ull << 31)) ? 1u : 0u;
+                        part_acc(S8, O8, ps, j, warm, (int32_t)e);
+                    };
+                    residuals_lpc<LPW, ST>(s, hs, c, (uint32_t)shq, q, l, acc);
+                    if (__any(bad)) continue;
+                    uint8_t *pb = par + (cur ^ 1u) * 512u;
+                    uint32_t best_o, best_m;
+                    const uint64_t rb = rice_search(S8, O8, q, P, pb, best_o, best_m);
+                    const uint64_t tot = rb + (uint64_t)q * (bps + (uint32_t)kLpcPrec) + 9u;
+                    if (tot < R.est) {
+                        R.type = 3;
+                        R.est = tot;
+                        R.order = q;
+                        R.porder = best_o;
+                        R.method = best_m;
+                        R.lsh = shq;
+                        cur ^= 1u;
+                    }
+                }
             }
         }
         STAMP(5);
@@ -1031,10 +1284,11 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                 // residuals were not kept through the search (register pressure): reload the
                 // samples from the staged PCM and recompute them.
                 const uint32_t o = R.porder, param_len = 4u + R.method, w = R.waste;
-                const uint8_t *pp = par + ((1u << o) - 1u);
+                const uint8_t *pp = par + cur * 512u + ((1u << o) - 1u);
                 if (l == 0) {
                     const uint32_t p0 = pp[0];
                     seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
+                    if (R.type == 3) seg += 4u + 5u + k * (uint32_t)kLpcPrec;  // precision, shift, coefficients
                 }
                 ST t[64];
                 load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, t);
@@ -1043,6 +1297,19 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                     for (int j = 0; j < 64; j++) t[j] >>= w;
                 }
                 const ST g1 = shr1(t[63]), g2 = shr1(t[62]), g3 = shr1(t[61]), g4 = shr1(t[60]);
+                // LPC residuals of the chosen order from the coefficient table (build-defined)
+                auto lpc_len_pass = [&](const ST (&tt)[64], auto &&f) {
+                    if constexpr (LPW > 0) {
+                        ST hs[LPW];
+#pragma unroll
+                        for (int q = 0; q < LPW; q++) hs[q] = shr1(tt[63 - q]);
+                        int32_t c[LPW];
+#pragma unroll
+                        for (int q = 0; q < LPW; q++) c[q] = __builtin_amdgcn_readfirstlane(ltab[(k - 1u) * 13u + q]);
+                        residuals_lpc<LPW, ST>(tt, hs, c, (uint32_t)R.lsh, k, l,
+                                               [&](int j, bool warm, int64_t e) { f(j, warm, (ST)(int32_t)e); });
+                    }
+                };
                 if constexpr (FULL) {
                     const uint32_t sh = 12u - o, psz = 4096u >> o;
                     uint32_t pq[4];
@@ -1059,7 +1326,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                         const uint32_t cl = esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
                         sg[j & 1] = add_chain(sg[j & 1], warm ? 0u : cl);
                     };
-                    FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, len_a)))
+                    if (LPW > 0 && R.type == 3) lpc_len_pass(t, len_a);
+                    else FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, len_a)))
                     seg = sg[0] + sg[1];
                 } else {
                     const uint32_t psz = n >> o;
@@ -1073,7 +1341,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                             seg += esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
                         }
                     };
-                    FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, len_a)))
+                    if (LPW > 0 && R.type == 3) lpc_len_pass(t, len_a);
+                    else FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, len_a)))
                 }
             }
         }
@@ -1083,7 +1352,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
 
         // ---- 11. the frame descriptor
         uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
-        const uint8_t *pp = par + ((1u << R.porder) - 1u);
+        const uint8_t *pp = par + cur * 512u + ((1u << R.porder) - 1u);
         if (my_slot >= 0) {
             SubDesc *sd = (SubDesc *)(fd + sizeof(FrameDesc)) + my_slot;
             if (l == 0) {
@@ -1096,9 +1365,14 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                 sd->cand = (uint8_t)cand;
                 sd->bits = sub_bits;
                 sd->cval = R.cval;
+                sd->lpc_shift = (int8_t)R.lsh;
+                sd->lpc_prec = (uint32_t)kLpcPrec;
+            }
+            if constexpr (LPW > 0) {
+                if (R.type == 3 && l < (uint32_t)kLpcMax) sd->coef[l] = (int16_t)ltab[(R.order - 1u) * 13u + l];
             }
             sd->lane_bits[l] = seg;
-            if (R.type == 2) {
+            if (R.type >= 2) {
                 const uint32_t np = 1u << R.porder;
                 for (uint32_t j = l; j < np; j += 64) sd->params[j] = pp[j];
             }
@@ -1137,9 +1411,18 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
                 sr->pad2 = 0;
                 sr->estimate = R.est;
                 sr->constant = R.cval;
+                sr->lpc_precision = R.type == 3 ? (uint8_t)kLpcPrec : 0;
+                sr->lpc_shift = R.type == 3 ? (int8_t)R.lsh : 0;
+            }
+            if (l < 32u) {
+                int32_t cv = 0;
+                if constexpr (LPW > 0) {
+                    if (R.type == 3 && l < (uint32_t)kLpcMax) cv = ltab[(R.order - 1u) * 13u + l];
+                }
+                sr->lpc_coefs[l] = cv;
             }
             const uint32_t np = 1u << R.porder;
-            for (uint32_t j = l; j < 256u; j += 64) sr->params[j] = (R.type == 2 && j < np) ? pp[j] : 0;
+            for (uint32_t j = l; j < 256u; j += 64) sr->params[j] = (R.type >= 2 && j < np) ? pp[j] : 0;
             if (tid == 0) {
                 fr->channel_code = channel_code;
                 fr->n_cand = NW;
@@ -1167,8 +1450,9 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL) ? FG
 // (frame_writer.zig:111-125,144-148) and stores the frame at its final byte
 // offset in the output bitstream.
 // ------------------------------------------------------------------------
-template <int B, int CLS, bool FULL, int MAXT, int NC>
-__global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL) ? FG_PACK_MINW : 2)) k_pack(EncodeArgs a) {
+template <int B, int CLS, bool FULL, int MAXT, int NC, int LPW>
+__global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PACK_MINW : 2)) k_pack(EncodeArgs a) {
+    constexpr int KW = LPW > 4 ? LPW : 4;  // most warm-up samples of any predictor
     using ST = typename Cls<CLS>::S;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
@@ -1238,6 +1522,17 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL) ? FG_PACK_MINW : 2)
             auto none = [](int, bool, ST) {};
             residuals_generic<ST>(s, h1, h2, h3, h4, l, k, none);
         }
+        if constexpr (LPW > 0) {
+            if (type == 3) {  // LPC (build-defined): coefficients from the descriptor
+                ST hs[LPW];
+#pragma unroll
+                for (int t = 0; t < LPW; t++) hs[t] = shr1(s[63 - t]);
+                int32_t c[LPW];
+#pragma unroll
+                for (int t = 0; t < LPW; t++) c[t] = (t < kLpcMax) ? __builtin_amdgcn_readfirstlane((int32_t)sd->coef[t < kLpcMax ? t : 0]) : 0;
+                residuals_lpc_inplace<LPW, ST>(s, hs, c, (uint32_t)(int32_t)sd->lpc_shift, k, l);
+            }
+        }
 
         // ---- 3. pack: each lane writes its contiguous bit segment (frame_writer.zig:269-372).
         // Every field is ORed into the zeroed image at its bit position; the per-sample
@@ -1252,13 +1547,21 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL) ? FG_PACK_MINW : 2)
                     bw.put(0, 8);
                     bw.put(((uint64_t)sd->cval << w) & (~0ull >> (64 - bd)), bd);
                 } else {
-                    const uint32_t hdr = (type == 1) ? (w ? 0x03u : 0x02u) : (((8u | k) << 1) | (w ? 1u : 0u));
-                    bw.put(hdr, 8);
+                    // type code: VERBATIM 1, FIXED 8|k, LPC 0x20|(k-1) (build-defined)
+                    const uint32_t tc = (type == 1) ? 1u : (type == 2 ? (8u | k) : (0x20u | (k - 1u)));
+                    bw.put((tc << 1) | (w ? 1u : 0u), 8);
                     if (w) bw.put(1, w);
-                    if (type == 2) {
+                    if (type >= 2) {
 #pragma unroll
-                        for (int j = 0; j < 4; j++)  // warm-up samples
+                        for (int j = 0; j < KW; j++)  // warm-up samples
                             if ((uint32_t)j < k) bw.put((uint64_t)(int64_t)s[j] & mask, bps);
+                        if (type == 3) {
+                            const uint32_t prec = sd->lpc_prec;
+                            bw.put(prec - 1u, 4);
+                            bw.put((uint32_t)(int32_t)sd->lpc_shift & 31u, 5);
+                            for (uint32_t t = 0; t < k; t++)
+                                bw.put((uint64_t)(int64_t)sd->coef[t] & (~0ull >> (64 - prec)), prec);
+                        }
                         bw.put((method << 4) | o, 6);
                         const uint32_t p0 = sd->params[0];
                         if (p0 & 0x80u) {
@@ -1278,7 +1581,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL) ? FG_PACK_MINW : 2)
                     put_or2(img, pos, (uint64_t)(int64_t)s[j] & mask, ok ? bps : 0u);
                     pos += ok ? bps : 0u;
                 }
-            } else if (type == 2) {
+            } else if (type >= 2) {
                 const uint32_t param_len = 4u + method;
                 const uint32_t esc_code = (0x0Fu | (method << 4)) << 5;
                 const uint8_t *pp = sd->params;
@@ -1312,7 +1615,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL) ? FG_PACK_MINW : 2)
 #pragma unroll
                         for (int jj = 0; jj < 16; jj++) {
                             const int j = 16 * q + jj;
-                            code((int32_t)s[j], p, j < 4 && l == 0 && (uint32_t)j < k);
+                            code((int32_t)s[j], p, j < KW && l == 0 && (uint32_t)j < k);
                         }
                     }
                 } else {
@@ -1422,16 +1725,16 @@ static hipError_t launch_persistent(KernelT k, const EncodeArgs &a, uint32_t thr
 
 // NC = 2 for two channels, 1 for mono, 0 (runtime) otherwise; MAXT by wave count.
 // stage: 0 = analysis, 1 = pack.
-template <int B, int CLS>
+template <int B, int CLS, int LPW>
 static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds,
                                  hipStream_t st) {
 #define FG_L(NCV, MT)                                                                                     \
     do {                                                                                                  \
         if (stage == 0)                                                                                   \
-            return full ? launch_persistent(k_analyze<B, CLS, true, MT, NCV>, a, threads, lds, st)       \
-                        : launch_persistent(k_analyze<B, CLS, false, MT, NCV>, a, threads, lds, st);     \
-        return full ? launch_persistent(k_pack<B, CLS, true, MT, NCV>, a, threads, lds, st)              \
-                    : launch_persistent(k_pack<B, CLS, false, MT, NCV>, a, threads, lds, st);            \
+            return full ? launch_persistent(k_analyze<B, CLS, true, MT, NCV, LPW>, a, threads, lds, st)  \
+                        : launch_persistent(k_analyze<B, CLS, false, MT, NCV, LPW>, a, threads, lds, st); \
+        return full ? launch_persistent(k_pack<B, CLS, true, MT, NCV, LPW>, a, threads, lds, st)         \
+                    : launch_persistent(k_pack<B, CLS, false, MT, NCV, LPW>, a, threads, lds, st);       \
     } while (0)
     if (a.channels == 2) FG_L(2, 256);
     if (a.channels == 1) FG_L(1, 256);

@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "fg_common.hpp"
+
 namespace fg {
 
 // Analysis kernel (one wave per candidate, nw waves).
@@ -10,7 +12,10 @@ struct AnaLayout {
     uint32_t stage1; // second staging buffer (double-buffered LDS-DMA prefetch), or == stage0
     uint32_t psum;   // tail kernel only: 2 x 256 u64 per wave
     uint32_t pmax;   // tail kernel only: 2 x 256 u32 per wave
-    uint32_t par;    // rice params, 512 B per candidate wave (orders 0..8 at offset (1<<o)-1)
+    uint32_t par;    // rice params, 512 B per candidate wave (orders 0..8 at offset (1<<o)-1);
+                     // with LPC two such buffers per wave (current best / candidate)
+    uint32_t par_stride;
+    uint32_t lpc;    // LPC: quantised coefficient table, kLpcTab i32 per wave
     uint32_t rec;    // 16 x u32 per candidate wave
     uint32_t misc;   // 64 x u32 scratch (header words)
     uint32_t total;
@@ -43,7 +48,8 @@ __host__ __device__ inline uint32_t stage_bytes(uint32_t C, uint32_t B) {
 // The full-frame kernel double-buffers it when both buffers fit and DMAs the
 // next frame's PCM into the idle one; the tail kernel (and configs whose two
 // buffers do not fit) stage synchronously into one buffer.
-__host__ __device__ inline AnaLayout ana_layout(uint32_t C, uint32_t B, uint32_t nw, bool full, bool dbuf) {
+__host__ __device__ inline AnaLayout ana_layout(uint32_t C, uint32_t B, uint32_t nw, bool full, bool dbuf,
+                                                bool lpc = false) {
     AnaLayout L;
     const uint32_t sb = fg_round16(stage_bytes(C, B));
     uint32_t end = sb;
@@ -58,7 +64,9 @@ __host__ __device__ inline AnaLayout ana_layout(uint32_t C, uint32_t B, uint32_t
         end += nw * 6144u;
     }
     L.par = end;
-    L.rec = L.par + nw * 512u;
+    L.par_stride = lpc ? 1024u : 512u;
+    L.lpc = L.par + nw * L.par_stride;
+    L.rec = L.lpc + (lpc ? nw * 4u * (uint32_t)kLpcTab : 0u);
     L.misc = L.rec + nw * 64u;
     L.total = fg_round16(L.misc + 256u);
     return L;

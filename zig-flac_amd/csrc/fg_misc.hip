@@ -10,20 +10,33 @@ namespace fg {
 
 __device__ __forceinline__ uint32_t lane_id_m() { return __lane_id(); }
 
-hipError_t launch_stage_b1(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
-hipError_t launch_stage_b2(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
-hipError_t launch_stage_b3(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
-hipError_t launch_stage_b4(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
+#define FG_DECL(B, W) \
+    hipError_t launch_stage_b##B##_l##W(int, const EncodeArgs &, bool, uint32_t, uint32_t, hipStream_t);
+#define FG_DECL3(B) FG_DECL(B, 0) FG_DECL(B, 8) FG_DECL(B, 12)
+FG_DECL3(1)
+FG_DECL3(2)
+FG_DECL3(3)
+FG_DECL3(4)
+
+// LPC taps held in registers for a configured maximum LPC order (0 = fixed only)
+uint32_t lpc_taps(uint32_t lpc_order) { return lpc_order == 0 ? 0u : (lpc_order <= 8 ? 8u : 12u); }
 
 // stage 0: analysis kernel, 1: pack kernel
 hipError_t launch_stage(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st) {
+    const uint32_t w = lpc_taps(a.lpc_order);
+#define FG_CASE(B)                                                                              \
+    case B:                                                                                     \
+        if (w == 0) return launch_stage_b##B##_l0(stage, a, full, threads, lds, st);            \
+        if (w == 8) return launch_stage_b##B##_l8(stage, a, full, threads, lds, st);            \
+        return launch_stage_b##B##_l12(stage, a, full, threads, lds, st);
     switch (a.bytes_per_sample) {
-        case 1: return launch_stage_b1(stage, a, full, threads, lds, st);
-        case 2: return launch_stage_b2(stage, a, full, threads, lds, st);
-        case 3: return launch_stage_b3(stage, a, full, threads, lds, st);
-        case 4: return launch_stage_b4(stage, a, full, threads, lds, st);
+        FG_CASE(1)
+        FG_CASE(2)
+        FG_CASE(3)
+        FG_CASE(4)
         default: return hipErrorInvalidValue;
     }
+#undef FG_CASE
 }
 
 // ------------------------------------------------------------------------

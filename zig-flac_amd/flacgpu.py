@@ -70,6 +70,10 @@ class SubframeRecord(ctypes.Structure):
         ("estimate", ctypes.c_uint64),
         ("constant", ctypes.c_int64),
         ("params", ctypes.c_uint8 * 256),
+        ("lpc_precision", ctypes.c_uint8),
+        ("lpc_shift", ctypes.c_int8),
+        ("pad3", ctypes.c_uint8 * 6),
+        ("lpc_coefs", ctypes.c_int32 * 32),
     ]
 
 
@@ -247,10 +251,10 @@ class Encoder:
 
     def __init__(self, channels: int, bits: int, sample_rate: int, device: int = 0, max_frames: int = 32768,
                  block_size: int = 4096, stereo_decorrelation: bool = True, max_rice_part_order: int = 8,
-                 max_rice_param: int = 30):
+                 max_rice_param: int = 30, lpc_order: int = 0):
         self.lib = load_library()
         self.cfg = Config(sample_rate, block_size, channels, bits, 1 if stereo_decorrelation else 0,
-                          max_rice_part_order, max_rice_param, 0)
+                          max_rice_part_order, max_rice_param, lpc_order)
         self.channels, self.bits, self.sample_rate, self.block_size = channels, bits, sample_rate, block_size
         self.bytes_per_sample = bits // 8
         self.max_frames = max_frames
