@@ -43,6 +43,8 @@ sys.path.insert(0, os.path.join(ROOT, "zig-flac_amd"))
 
 METRIC = "MSamples/s encoded (whole node), 44.1kHz/16-bit stereo, blocksize 4096"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# BASELINE.json configs (channels, bits, rate, LPC max order); c2 is the headline metric's
+PRESETS = {"c2": (2, 16, 44100, 0), "c3": (2, 24, 96000, 8), "c4": (8, 24, 96000, 0), "c5": (2, 32, 192000, 12)}
 
 
 def parse():
@@ -55,12 +57,18 @@ def parse():
     p.add_argument("--channels", type=int, default=2)
     p.add_argument("--bits", type=int, default=16)
     p.add_argument("--rate", type=int, default=44100)
+    p.add_argument("--lpc", type=int, default=0, help="LPC max order (0 = fixed prediction, the reference)")
+    p.add_argument("--config", choices=sorted(PRESETS), default=None,
+                   help="BASELINE.json config preset (overrides --channels/--bits/--rate/--lpc); default c2")
     p.add_argument("--no-md5", action="store_true", help="skip the per-stream GPU MD5 (diagnostics only)")
     p.add_argument("--cpu-frames", type=int, default=32768, help="blocks in the CPU-baseline sample")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--verify", action="store_true", help="decode + check a sample of streams after timing")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.config:
+        a.channels, a.bits, a.rate, a.lpc = PRESETS[a.config]
+    return a
 
 
 def make_pool(n, ch, bits, rate):
@@ -112,7 +120,7 @@ def cpu_baseline(buf, offsets, samples, args):
             blocks += nb
             s += args.cpu_threads
         jobs.append(mine)
-    cfg = oracle_ref.config(ch, bits, args.rate)
+    cfg = oracle_ref.config(ch, bits, args.rate, lpc=args.lpc)
     res = [0] * len(jobs)
 
     def run(i):
@@ -186,7 +194,7 @@ def main():
         raise SystemExit("--frames must be a multiple of --streams")
     buf, offsets, samples = build_input(args, rank)
     enc = flacgpu.Encoder(args.channels, args.bits, args.rate, device=torch.cuda.current_device(),
-                          max_frames=args.frames)
+                          max_frames=args.frames, lpc_order=args.lpc)
     plan = enc.plan(offsets, samples)
     d_pcm = torch.from_numpy(buf).to(dev)
     out_cap = int(plan.out_bound)
@@ -283,9 +291,12 @@ def main():
             "dtype": "int32",
             "data": "synthetic",
             "config": {
-                "workload": f"C2: {args.rate/1000:g}kHz {args.bits}-bit {args.channels}ch, blocksize 4096, "
+                "workload": f"{(args.config or 'c2').upper()}: {args.rate/1000:g}kHz {args.bits}-bit "
+                            f"{args.channels}ch, blocksize 4096, "
                             f"{args.frames} blocks/GPU as {args.streams} streams x {args.frames // args.streams} "
-                            f"blocks, fixed prediction, per-stream GPU MD5{' (off)' if args.no_md5 else ''}",
+                            f"blocks, " + (f"LPC orders 1..{args.lpc} + full subframe-type search"
+                                           if args.lpc else "fixed prediction") +
+                            f", per-stream GPU MD5{' (off)' if args.no_md5 else ''}",
                 "blocks_per_gpu": args.frames,
                 "streams_per_gpu": args.streams,
                 "samples_per_gpu": samples_per_rank,

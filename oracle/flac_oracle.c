@@ -393,6 +393,8 @@ static void calc_residuals(const int64_t *s, uint32_t n, unsigned k, int wide, i
 /* lists it as in progress; Prediction = {fixed, none}, encoder.zig:629-640;*/
 /* the `linear` subframe is commented out, encoder.zig:694-699), so this is */
 /* the contract the gfx950 kernels share with this restatement bit for bit: */
+/*  0. LPC is searched on i32 samples only (a 32-bit stereo side that     */
+/*     still needs 33 bits after its waste shift keeps its fixed choice);  */
 /*  1. window w(i) = (i+1)(n-i): integer, Welch-shaped, never zero;        */
 /*  2. xw(i) = (x(i) w(i)) >> sh (arithmetic), sh = max(0, bitlen(max|x|)  */
 /*     + bitlen(floor((n+1)^2/4)) - 25), so |xw| <= 2^25;                 */
@@ -527,6 +529,8 @@ static unsigned calc_waste(int64_t *s, uint32_t n, unsigned bps) {
 static void lpc_search(sub_t *sub, const int64_t *s, uint32_t n, const oracle_config *cfg, unsigned bps,
                        unsigned Q) {
     oracle_subframe *r = &sub->rec;
+    for (uint32_t i = 0; i < n; i++)
+        if (s[i] != (int64_t)(int32_t)s[i]) return; /* 33-bit side: no LPC (contract step 0) */
     int64_t R[ORACLE_LPC_MAX_ORDER + 1];
     static __thread double coefs[ORACLE_LPC_MAX_ORDER * ORACLE_LPC_MAX_ORDER];
     oracle_lpc_autocorr(s, n, Q, R);

@@ -510,6 +510,53 @@ __device__ __forceinline__ void load_candidate(const uint32_t *stg, uint32_t cst
     }
 }
 
+// Samples of candidate `cand` for the LPC search, as i32 after the waste shift w: the
+// build-defined LPC works on i32 samples, so a 32-bit stereo side that still needs 33
+// bits after its shift skips LPC.  Returns false on a lane holding such a sample.
+template <int B, int CLS, bool FULL, int NC>
+__device__ __forceinline__ bool load_lpc_samples(const uint32_t *stg, uint32_t cst, uint32_t l, uint32_t n,
+                                                 bool stereo, uint32_t cand, uint32_t C, uint32_t w,
+                                                 int32_t (&x)[64]) {
+    if constexpr (CLS != 32) {
+        load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, x);
+        if (w != 0) {
+#pragma unroll
+            for (int j = 0; j < 64; j++) x[j] >>= w;
+        }
+        return true;
+    } else {
+        const uint32_t *lw = stg + l * cst;
+        const uint32_t kind = stereo ? cand : 0u;
+        const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand;
+        bool fits = true;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) {
+                const int j = 16 * g + jj;
+                int64_t L, Rr;
+                if constexpr (NC == 2) {
+                    const uint2 v = ((const uint2 *)lw)[j];
+                    L = (int32_t)(chan ? v.y : v.x);
+                    Rr = (int32_t)v.y;
+                    if (kind >= 2) L = (int32_t)v.x;
+                } else {
+                    const uint8_t *base = (const uint8_t *)lw;
+                    L = ld_sample<4>(base + j * C * 4u + chan * 4u);
+                    Rr = 0;
+                }
+                int64_t v = kind <= 1 ? L : (kind == 2 ? (L + Rr) >> 1 : L - Rr);
+                if (!FULL && l * 64u + j >= n) v = 0;
+                v >>= w;
+                fits &= v == (int64_t)(int32_t)v;
+                x[j] = (int32_t)v;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return fits;
+    }
+}
+
 // Fixed-predictor residual of order K from sample x and history q1..q4
 // (fixed.zig:12-18 COEFF_SCALAR stencil): wrapping i32 (narrow, fixed.zig:63-68)
 // or exact i64 truncated to i32 (wide, fixed.zig:69-74).
@@ -621,6 +668,7 @@ __device__ __forceinline__ void lpc_autocorr(const ST (&s)[64], uint32_t n, uint
             const int32_t y = (j - g >= 0) ? xv[(j - g) >= 0 ? (j - g) : 0] : hx[(g - j - 1) >= 0 ? (g - j - 1) : 0];
             acc[g] += (int64_t)xv[j] * (int64_t)y;
         }
+        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int g = 0; g <= W; g++) R[g] = (int64_t)wave_sum64((uint64_t)acc[g]);
@@ -725,6 +773,7 @@ __device__ __forceinline__ void residuals_lpc(const ST (&s)[64], const ST (&hs)[
         const int64_t e = (int64_t)s[j] - (lpc_pred<W, ST>(s, hs, c, j) >> shift);
         const bool warm = (j < W) && (l == 0) && ((uint32_t)j < q);
         f(j, warm, e);
+        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound the scheduler's hoisting
     }
 }
 
@@ -738,6 +787,7 @@ __device__ __forceinline__ void residuals_lpc_inplace(ST (&s)[64], const ST (&hs
         const int64_t e = (int64_t)s[j] - (lpc_pred<W, ST>(s, hs, c, j) >> shift);
         const bool warm = (j < W) && (l == 0) && ((uint32_t)j < q);
         if (!warm) s[j] = (ST)(int32_t)e;
+        if ((j & 7) == 0) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -1185,47 +1235,59 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             ltab = (int32_t *)(smem + LY.lpc) + wave * (uint32_t)kLpcTab;
             const uint32_t Q = a.lpc_order;
             if (lpc_on && R.type != 0 && n > Q) {
+                bool fits;
                 {
-                    int64_t Rac[LPW + 1];
-                    lpc_autocorr<LPW, ST>(s, n, l, Rac);
-                    lpc_coefs<LPW>(Rac, Q, ltab, l == 0);
+                    int32_t x[64];
+                    fits = __all(load_lpc_samples<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, R.waste, x));
+                    if (fits) {
+                        int64_t Rac[LPW + 1];
+                        lpc_autocorr<LPW, int32_t>(x, n, l, Rac);
+                        __builtin_amdgcn_sched_barrier(0);
+                        lpc_coefs<LPW>(Rac, Q, ltab, l == 0);
+                    }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                ST hs[LPW];
+                if (fits) {
+                    // the samples again (not held through Levinson-Durbin: register pressure)
+                    int32_t x[64];
+                    (void)load_lpc_samples<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, R.waste, x);
+                    int32_t hs[LPW];
 #pragma unroll
-                for (int t = 0; t < LPW; t++) hs[t] = shr1(s[63 - t]);
-                for (uint32_t q = 1; q <= Q; q++) {
-                    const int32_t shq = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + 12u]);
-                    if (shq < 0) continue;
-                    int32_t c[LPW];
+                    for (int t = 0; t < LPW; t++) hs[t] = shr1(x[63 - t]);
+                    for (uint32_t q = 1; q <= Q; q++) {
+                        const int32_t shq = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + 12u]);
+                        if (shq < 0) continue;
+                        int32_t c[LPW];
 #pragma unroll
-                    for (int t = 0; t < LPW; t++) c[t] = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + t]);
-                    SumT S8[4] = {0, 0, 0, 0};
-                    uint32_t O8[4] = {0, 0, 0, 0};
-                    const uint32_t P = part_cap(q);
-                    const uint32_t ps = n >> P;
-                    zero_parts();
-                    uint32_t bad = 0;
-                    auto acc = [&](int j, bool warm, int64_t e) {
-                        // usable only if every coded residual's zigzag fits 31 bits
-                        const bool valid = !warm && (FULL || l * 64u + (uint32_t)j < n);
-                        bad |= (valid && (uint64_t)(e + (1ll << 30)) >= (1ull << 31)) ? 1u : 0u;
-                        part_acc(S8, O8, ps, j, warm, (int32_t)e);
-                    };
-                    residuals_lpc<LPW, ST>(s, hs, c, (uint32_t)shq, q, l, acc);
-                    if (__any(bad)) continue;
-                    uint8_t *pb = par + (cur ^ 1u) * 512u;
-                    uint32_t best_o, best_m;
-                    const uint64_t rb = rice_search(S8, O8, q, P, pb, best_o, best_m);
-                    const uint64_t tot = rb + (uint64_t)q * (bps + (uint32_t)kLpcPrec) + 9u;
-                    if (tot < R.est) {
-                        R.type = 3;
-                        R.est = tot;
-                        R.order = q;
-                        R.porder = best_o;
-                        R.method = best_m;
-                        R.lsh = shq;
-                        cur ^= 1u;
+                        for (int t = 0; t < LPW; t++)
+                            c[t] = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + t]);
+                        SumT S8[4] = {0, 0, 0, 0};
+                        uint32_t O8[4] = {0, 0, 0, 0};
+                        const uint32_t P = part_cap(q);
+                        const uint32_t ps = n >> P;
+                        zero_parts();
+                        uint32_t bad = 0;
+                        auto acc = [&](int j, bool warm, int64_t e) {
+                            // usable only if every coded residual's zigzag fits 31 bits
+                            const bool valid = !warm && (FULL || l * 64u + (uint32_t)j < n);
+                            bad |= (valid && (uint64_t)(e + (1ll << 30)) >= (1ull << 31)) ? 1u : 0u;
+                            part_acc(S8, O8, ps, j, warm, (int32_t)e);
+                        };
+                        residuals_lpc<LPW, int32_t>(x, hs, c, (uint32_t)shq, q, l, acc);
+                        if (__any(bad)) continue;
+                        uint8_t *pb = par + (cur ^ 1u) * 512u;
+                        uint32_t best_o, best_m;
+                        const uint64_t rb = rice_search(S8, O8, q, P, pb, best_o, best_m);
+                        const uint64_t tot = rb + (uint64_t)q * (bps + (uint32_t)kLpcPrec) + 9u;
+                        if (tot < R.est) {
+                            R.type = 3;
+                            R.est = tot;
+                            R.order = q;
+                            R.porder = best_o;
+                            R.method = best_m;
+                            R.lsh = shq;
+                            cur ^= 1u;
+                        }
                     }
                 }
             }
@@ -1290,24 +1352,32 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
                     if (R.type == 3) seg += 4u + 5u + k * (uint32_t)kLpcPrec;  // precision, shift, coefficients
                 }
-                ST t[64];
-                load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, t);
-                if (w != 0) {
+                // residuals of the chosen predictor, recomputed from the staged PCM: fixed order k
+                // (fixed.zig:30-76) or the chosen LPC order from the coefficient table
+                auto pass = [&](auto &&f) {
+                    if (LPW > 0 && R.type == 3) {
+                        if constexpr (LPW > 0) {
+                            int32_t x[64];
+                            (void)load_lpc_samples<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, w, x);
+                            int32_t hs[LPW];
 #pragma unroll
-                    for (int j = 0; j < 64; j++) t[j] >>= w;
-                }
-                const ST g1 = shr1(t[63]), g2 = shr1(t[62]), g3 = shr1(t[61]), g4 = shr1(t[60]);
-                // LPC residuals of the chosen order from the coefficient table (build-defined)
-                auto lpc_len_pass = [&](const ST (&tt)[64], auto &&f) {
-                    if constexpr (LPW > 0) {
-                        ST hs[LPW];
+                            for (int q = 0; q < LPW; q++) hs[q] = shr1(x[63 - q]);
+                            int32_t c[LPW];
 #pragma unroll
-                        for (int q = 0; q < LPW; q++) hs[q] = shr1(tt[63 - q]);
-                        int32_t c[LPW];
+                            for (int q = 0; q < LPW; q++)
+                                c[q] = __builtin_amdgcn_readfirstlane(ltab[(k - 1u) * 13u + q]);
+                            residuals_lpc<LPW, int32_t>(x, hs, c, (uint32_t)R.lsh, k, l,
+                                                        [&](int j, bool warm, int64_t e) { f(j, warm, (ST)(int32_t)e); });
+                        }
+                    } else {
+                        ST t[64];
+                        load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, t);
+                        if (w != 0) {
 #pragma unroll
-                        for (int q = 0; q < LPW; q++) c[q] = __builtin_amdgcn_readfirstlane(ltab[(k - 1u) * 13u + q]);
-                        residuals_lpc<LPW, ST>(tt, hs, c, (uint32_t)R.lsh, k, l,
-                                               [&](int j, bool warm, int64_t e) { f(j, warm, (ST)(int32_t)e); });
+                            for (int j = 0; j < 64; j++) t[j] >>= w;
+                        }
+                        const ST g1 = shr1(t[63]), g2 = shr1(t[62]), g3 = shr1(t[61]), g4 = shr1(t[60]);
+                        FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, f)))
                     }
                 };
                 if constexpr (FULL) {
@@ -1326,8 +1396,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                         const uint32_t cl = esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
                         sg[j & 1] = add_chain(sg[j & 1], warm ? 0u : cl);
                     };
-                    if (LPW > 0 && R.type == 3) lpc_len_pass(t, len_a);
-                    else FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, len_a)))
+                    pass(len_a);
                     seg = sg[0] + sg[1];
                 } else {
                     const uint32_t psz = n >> o;
@@ -1341,8 +1410,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                             seg += esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
                         }
                     };
-                    if (LPW > 0 && R.type == 3) lpc_len_pass(t, len_a);
-                    else FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, len_a)))
+                    pass(len_a);
                 }
             }
         }
