@@ -54,7 +54,7 @@ def test_reference_max_frame_bytes():
 @pytest.mark.parametrize("field,value", [("bits_per_sample", 12), ("bits_per_sample", 20), ("channels", 0),
                                          ("channels", 9), ("block_size", 0), ("block_size", 8192),
                                          ("max_rice_part_order", 9), ("max_rice_param", 0), ("max_rice_param", 31),
-                                         ("prediction", 8), ("sample_rate", 1 << 20)])
+                                         ("prediction", 13), ("prediction", 32), ("sample_rate", 1 << 20)])
 def test_invalid_configs_rejected(field, value):
     lib = flacgpu.load_library()
     cfg = flacgpu.Config.default(2, 16, 44100)
