@@ -58,6 +58,19 @@ __global__ void __launch_bounds__(64) k_md5(const uint32_t *data, uint64_t words
         }
         out[s] = st[0] ^ st[1] ^ st[2] ^ st[3];
         out[s + n / 2] = su[0] ^ su[1] ^ su[2] ^ su[3];
+    } else if (V == 3) {
+        // 16 active lanes per wave (lanes 16..63 idle): does a partial exec mask issue faster?
+        const uint32_t lane = threadIdx.x;
+        const uint32_t s3 = blockIdx.x * 16 + lane;
+        if (lane >= 16 || s3 >= n) return;
+        const uint32_t *p = data + (uint64_t)s3 * words_per_stream;
+        uint32_t st[4] = {1, 2, 3, 4};
+        for (uint64_t b = 0; b < words_per_stream / 16; b++) {
+            uint32_t m[16];
+            for (int i = 0; i < 16; i++) m[i] = p[b * 16 + i];
+            compress<0>(st, m);
+        }
+        out[s3] = st[0] ^ st[1] ^ st[2] ^ st[3];
     } else {
         if (s >= n) return;
         const uint32_t *p = data + (uint64_t)s * words_per_stream;
@@ -81,13 +94,14 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    for (int v = 0; v < 3; v++) {
+    for (int v = 0; v < 4; v++) {
         for (int rep = 0; rep < 3; rep++) {
             hipEventRecord(e0);
-            uint32_t grid = (v == 1 ? n / 2 : n) / 64;
+            uint32_t grid = v == 3 ? n / 16 : (v == 1 ? n / 2 : n) / 64;
             if (v == 0) hipLaunchKernelGGL(k_md5<0>, dim3(grid), dim3(64), 0, 0, d, words, n, o);
             if (v == 1) hipLaunchKernelGGL(k_md5<1>, dim3(grid), dim3(64), 0, 0, d, words, n, o);
             if (v == 2) hipLaunchKernelGGL(k_md5<2>, dim3(grid), dim3(64), 0, 0, d, words, n, o);
+            if (v == 3) hipLaunchKernelGGL(k_md5<3>, dim3(grid), dim3(64), 0, 0, d, words, n, o);
             hipEventRecord(e1);
             hipEventSynchronize(e1);
             float ms;
