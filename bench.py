@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--config", choices=sorted(PRESETS), default=None,
                    help="BASELINE.json config preset (overrides --channels/--bits/--rate/--lpc); default c2")
     p.add_argument("--no-md5", action="store_true", help="skip the per-stream GPU MD5 (diagnostics only)")
+    p.add_argument("--md5-join", action="store_true",
+                   help="join each step's MD5 back into the encode stream (no overlap of consecutive steps)")
     p.add_argument("--cpu-frames", type=int, default=32768, help="blocks in the CPU-baseline sample")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
@@ -204,11 +206,18 @@ def main():
     d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
     d_md5 = torch.zeros(args.streams * 16, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # The MD5 is per-stream sequential (latency-bound), the encode throughput-bound: step k's MD5
+    # runs on its own HIP stream (two alternate) and overlaps step k+1's encode.  Every step's MD5
+    # and frames are complete at the synchronize that closes the timed region.
+    md5_streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    n_step = [0]
 
     def step():
+        ms = None if args.md5_join else md5_streams[n_step[0] % 2].cuda_stream
+        n_step[0] += 1
         enc.encode_plan_device(plan, d_pcm.data_ptr(), d_out.data_ptr(), out_cap, d_fb.data_ptr(),
                                d_off.data_ptr(), d_tot.data_ptr(), None if args.no_md5 else d_md5.data_ptr(),
-                               stream.cuda_stream)
+                               stream.cuda_stream, md5_stream=ms)
 
     for _ in range(args.warmup):
         step()
@@ -296,7 +305,9 @@ def main():
                             f"{args.frames} blocks/GPU as {args.streams} streams x {args.frames // args.streams} "
                             f"blocks, " + (f"LPC orders 1..{args.lpc} + full subframe-type search"
                                            if args.lpc else "fixed prediction") +
-                            f", per-stream GPU MD5{' (off)' if args.no_md5 else ''}",
+                            f", per-stream GPU MD5" + (" (off)" if args.no_md5 else
+                                                          (" joined per step" if args.md5_join else
+                                                           " overlapping the next step's encode")),
                 "blocks_per_gpu": args.frames,
                 "streams_per_gpu": args.streams,
                 "samples_per_gpu": samples_per_rank,

@@ -134,6 +134,18 @@ int flacgpu_encode_plan_device(flacgpu_ctx *ctx, const flacgpu_plan *plan, const
                                uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets,
                                uint64_t *d_total, uint8_t *d_md5, void *hip_stream);
 
+/* As flacgpu_encode_plan_device, but the MD5 of the streams is queued on
+ * md5_stream (after the PCM is ready on hip_stream) and NOT joined back into
+ * hip_stream: the encode of the next batch can start while this batch's MD5
+ * chains finish (the MD5 is per-stream sequential and latency-bound, the
+ * encode is throughput-bound, so consecutive batches overlap).  The caller
+ * synchronises md5_stream before reading d_md5 or reusing d_pcm.
+ * md5_stream == NULL behaves exactly like flacgpu_encode_plan_device. */
+int flacgpu_encode_plan_device_md5_async(flacgpu_ctx *ctx, const flacgpu_plan *plan, const void *d_pcm,
+                                         uint8_t *d_out, uint64_t out_cap, uint32_t *d_frame_bytes,
+                                         uint64_t *d_frame_offsets, uint64_t *d_total, uint8_t *d_md5,
+                                         void *hip_stream, void *md5_stream);
+
 /* ---- File level (host code around the GPU frame path) --------------------- */
 
 /* The context's configuration (what flacgpu_open was given). */

@@ -649,31 +649,43 @@ uint64_t flacgpu_plan_stream_first_frame(const flacgpu_plan *p, uint32_t s) {
     return (p && s < p->n_streams) ? p->first_frame[s] : 0;
 }
 
-int flacgpu_encode_plan_device(flacgpu_ctx *c, const flacgpu_plan *p, const void *d_pcm, uint8_t *d_out,
-                               uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets, uint64_t *d_total,
-                               uint8_t *d_md5, void *hip_stream) {
+int flacgpu_encode_plan_device_md5_async(flacgpu_ctx *c, const flacgpu_plan *p, const void *d_pcm, uint8_t *d_out,
+                                         uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets,
+                                         uint64_t *d_total, uint8_t *d_md5, void *hip_stream, void *md5_stream) {
     if (!c || !p || p->ctx != c || !d_pcm || !d_out || !d_frame_bytes || !d_frame_offsets || !d_total)
         return FLACGPU_ERR_INVALID_INPUT;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     if (c->records_on && p->n_frames > c->max_frames) return FLACGPU_ERR_INVALID_INPUT;
     uint8_t *desc = p->d_desc ? p->d_desc : c->d_desc;
-    // MD5 of every stream on the auxiliary stream, overlapping the encode kernels
+    // MD5 of every stream on a second stream, overlapping the encode kernels (joined back into
+    // st unless the caller owns the MD5 stream)
+    const bool join = md5_stream == nullptr;
+    hipStream_t ms = join ? c->aux : (hipStream_t)md5_stream;
     if (d_md5 && p->n_streams) {
-        HIPCHK(hipEventRecord(c->fork, st));
-        HIPCHK(hipStreamWaitEvent(c->aux, c->fork, 0));
+        hipEvent_t fork = join ? c->fork : get_event(c);
+        if (!fork) return FLACGPU_ERR_DEVICE;
+        HIPCHK(hipEventRecord(fork, st));
+        HIPCHK(hipStreamWaitEvent(ms, fork, 0));
+        if (!join) c->event_pool.push_back(fork);  // recycled: the wait is already enqueued
         {
-            Timed t(c, FLACGPU_K_MD5, c->aux);
-            HIPCHK(launch_md5_streams((const uint8_t *)d_pcm, p->d_md5_offs, p->d_md5_lens, p->n_streams, d_md5,
-                                      c->aux));
+            Timed t(c, FLACGPU_K_MD5, ms);
+            HIPCHK(launch_md5_streams((const uint8_t *)d_pcm, p->d_md5_offs, p->d_md5_lens, p->n_streams, d_md5, ms));
         }
-        HIPCHK(hipEventRecord(c->join, c->aux));
+        if (join) HIPCHK(hipEventRecord(c->join, ms));
     }
     int rc = encode_core(c, (const uint8_t *)d_pcm, p->d_jobs, p->n_full, p->n_tail, desc, d_frame_bytes, d_out,
                          out_cap, d_frame_offsets, d_total, st);
     if (rc) return rc;
-    if (d_md5 && p->n_streams) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
+    if (join && d_md5 && p->n_streams) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
     return FLACGPU_OK;
+}
+
+int flacgpu_encode_plan_device(flacgpu_ctx *c, const flacgpu_plan *p, const void *d_pcm, uint8_t *d_out,
+                               uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets, uint64_t *d_total,
+                               uint8_t *d_md5, void *hip_stream) {
+    return flacgpu_encode_plan_device_md5_async(c, p, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total,
+                                                d_md5, hip_stream, nullptr);
 }
 
 // ---- instrumentation ---------------------------------------------------------

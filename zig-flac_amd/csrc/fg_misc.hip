@@ -57,14 +57,28 @@ __global__ void k_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, 
 }
 
 // ------------------------------------------------------------------------
-// exclusive scan of frame sizes -> byte offsets (single workgroup, 1024 thr)
+// exclusive scan of frame sizes -> byte offsets (single workgroup, 1024 thr).
+// Thread t owns a contiguous run of `per` sizes (a multiple of 4), read as
+// 16-byte vectors and written back as 16-byte pairs of u64 offsets; the
+// thread totals are scanned across the workgroup with wave shuffles.
 // ------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n) {
     __shared__ uint64_t wsum[16];
-    const uint32_t t = threadIdx.x, per = (n + 1023u) / 1024u;
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (((n + 1023u) / 1024u) + 3u) & ~3u;
     const uint32_t b = t * per, e = min(n, b + per);
+    // 16-byte vectors only when both buffers are 16-byte aligned (caller-provided pointers)
+    const bool vec = ((reinterpret_cast<uintptr_t>(sizes) | reinterpret_cast<uintptr_t>(offsets)) & 15u) == 0;
     uint64_t acc = 0;
-    for (uint32_t i = b; i < e; i++) acc += sizes[i];
+    if (vec && b + per <= n) {
+        const uint4 *s4 = (const uint4 *)(sizes + b);
+        for (uint32_t i = 0; i < per / 4u; i++) {
+            const uint4 v = s4[i];
+            acc += (uint64_t)v.x + v.y + v.z + v.w;
+        }
+    } else {
+        for (uint32_t i = b; i < e; i++) acc += sizes[i];
+    }
     // block exclusive scan of acc
     uint64_t x = acc;
     const uint32_t l = lane_id_m(), w = t >> 6;
@@ -78,9 +92,24 @@ __global__ void __launch_bounds__(1024) k_scan(const uint32_t *sizes, uint64_t *
     uint64_t pre = 0;
     for (uint32_t i = 0; i < w; i++) pre += wsum[i];
     uint64_t run = pre + x - acc;
-    for (uint32_t i = b; i < e; i++) {
-        offsets[i] = run;
-        run += sizes[i];
+    if (vec && b + per <= n) {
+        const uint4 *s4 = (const uint4 *)(sizes + b);
+        ulonglong2 *o2 = (ulonglong2 *)(offsets + b);
+        for (uint32_t i = 0; i < per / 4u; i++) {
+            const uint4 v = s4[i];
+            ulonglong2 a, c;
+            a.x = run; run += v.x;
+            a.y = run; run += v.y;
+            c.x = run; run += v.z;
+            c.y = run; run += v.w;
+            o2[2 * i] = a;
+            o2[2 * i + 1] = c;
+        }
+    } else {
+        for (uint32_t i = b; i < e; i++) {
+            offsets[i] = run;
+            run += sizes[i];
+        }
     }
     if (t == 1023) {
         uint64_t tot = 0;
@@ -150,7 +179,10 @@ __global__ void __launch_bounds__(64) k_md5_streams(const uint8_t *base, const u
     if (s >= n_streams) return;
     // The chain is latency-bound (one dependent VALU op every issue slot) and these few
     // waves share SIMDs with the encode kernels: take issue priority over them.
-    __builtin_amdgcn_s_setprio(3);
+#ifndef FG_MD5_PRIO
+#define FG_MD5_PRIO 3
+#endif
+    __builtin_amdgcn_s_setprio(FG_MD5_PRIO);
     const uint8_t *p = base + offs[s];
     const uint64_t len = lens[s];
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};

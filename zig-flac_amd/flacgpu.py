@@ -177,6 +177,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_plan_out_bound": (U64, [P]),
         "flacgpu_plan_stream_first_frame": (U64, [P, U32]),
         "flacgpu_encode_plan_device": (I32, [P, P, P, P, U64, P, P, P, P, P]),
+        "flacgpu_encode_plan_device_md5_async": (I32, [P, P, P, P, U64, P, P, P, P, P, P]),
         "flacgpu_set_timing": (I32, [P, I32]),
         "flacgpu_kernel_time": (I32, [P, I32, ctypes.POINTER(U64), ctypes.POINTER(ctypes.c_double)]),
         "flacgpu_reset_timing": (I32, [P]),
@@ -206,7 +207,8 @@ def exported_symbols() -> list:
         "flacgpu_reference_max_frame_bytes", "flacgpu_frame_bound_bytes", "flacgpu_encode_frames",
         "flacgpu_encode_frame_planar", "flacgpu_md5_init", "flacgpu_md5_update", "flacgpu_md5_final",
         "flacgpu_plan_create", "flacgpu_plan_destroy", "flacgpu_plan_frames", "flacgpu_plan_out_bound",
-        "flacgpu_plan_stream_first_frame", "flacgpu_encode_plan_device", "flacgpu_set_timing",
+        "flacgpu_plan_stream_first_frame", "flacgpu_encode_plan_device", "flacgpu_encode_plan_device_md5_async",
+        "flacgpu_set_timing",
         "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_get_records",
         "flacgpu_get_config", "flacgpu_wav_parse", "flacgpu_streaminfo_init", "flacgpu_streaminfo_update_frame_size",
         "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file",
@@ -356,7 +358,14 @@ class Encoder:
 
     def encode_plan_device(self, plan: Plan, d_pcm: int, d_out: int, out_cap: int, d_frame_bytes: int,
                            d_frame_offsets: int, d_total: int, d_md5: Optional[int] = None,
-                           stream: Optional[int] = None) -> None:
+                           stream: Optional[int] = None, md5_stream: Optional[int] = None) -> None:
+        """md5_stream: queue the MD5 there without joining it back into `stream` (the caller
+        synchronises it); None joins it (flacgpu_encode_plan_device)."""
+        if md5_stream:
+            _check(self.lib.flacgpu_encode_plan_device_md5_async(
+                self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total,
+                d_md5 or None, stream or None, md5_stream), "encode_plan_device_md5_async")
+            return
         _check(self.lib.flacgpu_encode_plan_device(self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes,
                                                    d_frame_offsets, d_total, d_md5 or None, stream or None),
                "encode_plan_device")
