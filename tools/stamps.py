@@ -5,8 +5,9 @@ sys.path.insert(0, os.path.join(ROOT, "zig-flac_amd"))
 import numpy as np, torch
 import flacgpu, synth
 
-NAMES = ["stage wait", "sample load", "waste+eq", "bestOrder", "rice pass", "param search", "rec+zero barriers",
-         "hdr+passA+bar", "sub offsets", "pass B", "bar after B", "CRC+final", "copy+rec+bar"]
+NAMES = ["stage wait", "sample load", "waste+eq", "bestOrder", "rice pass", "param search", "desc+rec+bar",
+         "stereo+exact"]
+PNAMES = ["stage+bar", "load+offsets", "zero img+bars", "residuals", "pack codes+bar", "CRC+bars", "store+bar"]
 S, F = 1024, 32
 enc = flacgpu.Encoder(2, 16, 44100, max_frames=S * F)
 L = enc.lib
@@ -32,6 +33,9 @@ for _ in range(5):
 torch.cuda.synchronize()
 print("encode ms/launch", enc.kernel_time(0))
 L.flacgpu_debug_stamps(enc.ctx, out, 0)
-tot = sum(out[:13])
-for i, n in enumerate(NAMES):
-    print(f"{i:2d} {n:20s} {out[i] / max(tot,1) * 100:6.2f}%  {out[i] / (5 * S * F * 4):10.1f} clk/wave-frame")
+for base, names, label in [(0, NAMES, "analysis"), (16, PNAMES, "pack")]:
+    tot = sum(out[base:base + len(names)])
+    print(f"-- {label}")
+    for i, n in enumerate(names):
+        v = out[base + i]
+        print(f"{i:2d} {n:20s} {v / max(tot,1) * 100:6.2f}%  {v / (5 * S * F * (4 if base == 0 else 2)):10.1f} clk/wave-frame")

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -67,6 +68,7 @@ struct flacgpu_ctx {
     uint32_t C = 0, B = 0, bits = 0, stereo = 0, nt = 0, nt_pack = 0;
     uint32_t image_bytes = 0, desc_stride = 0, lds = 0, lds_tail = 0, lds_pack = 0, crc_hmax = 0;
     bool stage_dbuf = false;
+    bool pack_dbuf = false;
     hipStream_t stream = nullptr, aux = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr, *d_crc_join = nullptr;
@@ -208,6 +210,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.desc_stride = c->desc_stride;
     a.image_bytes = c->image_bytes;
     a.stage_dbuf = c->stage_dbuf ? 1u : 0u;
+    a.pack_dbuf = c->pack_dbuf ? 1u : 0u;
     a.frame_bytes = d_fbytes;
     a.offsets = d_offsets;
     a.out = d_out;
@@ -353,7 +356,12 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     c->stage_dbuf = ana_layout(c->C, c->B, nw, true, true, lpc).total <= 160u * 1024u;
     c->lds = ana_layout(c->C, c->B, nw, true, c->stage_dbuf, lpc).total;
     c->lds_tail = ana_layout(c->C, c->B, nw, false, false, lpc).total;
-    c->lds_pack = pack_layout(c->C, c->B, c->image_bytes).total;
+    // pack: double-buffer the staging when that keeps the register-limited occupancy
+    // (4 workgroups per CU; 2 for 32-bit samples)
+    const uint32_t pack_wgs = c->B == 4 ? 2u : 4u;
+    c->pack_dbuf = pack_layout(c->C, c->B, c->image_bytes, true).total * pack_wgs <= 160u * 1024u;
+    if (const char *e = std::getenv("FLACGPU_PACK_DBUF")) c->pack_dbuf = c->pack_dbuf && e[0] == '1';  // tuning knob
+    c->lds_pack = pack_layout(c->C, c->B, c->image_bytes, c->pack_dbuf).total;
     // CRC fold: half-segments of H words (odd), H <= ceil(image words / (2 * pack threads))
     c->crc_hmax = ((c->image_bytes / 4u + 2u * c->nt_pack - 1u) / (2u * c->nt_pack)) | 1u;
     if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u) {
@@ -370,10 +378,11 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
 
-    // CRC-16 tables: x * z^e mod P for e = 40, 32, 24, 16 (see crc_word in the kernels)
-    std::vector<uint16_t> tab(1024);
-    const uint32_t ze[4] = {crc_zpow(40), crc_zpow(32), crc_zpow(24), crc_zpow(16)};
-    for (int t = 0; t < 4; t++)
+    // CRC-16 tables: x * z^e mod P for e = 40, 32, 24, 16, 72, 64, 56, 48 (crc_word / crc_word2)
+    std::vector<uint16_t> tab(2048);
+    const uint32_t ze[8] = {crc_zpow(40), crc_zpow(32), crc_zpow(24), crc_zpow(16),
+                            crc_zpow(72), crc_zpow(64), crc_zpow(56), crc_zpow(48)};
+    for (int t = 0; t < 8; t++)
         for (uint32_t x = 0; x < 256; x++) tab[t * 256 + x] = (uint16_t)crc_mulmod_host(x, ze[t]);
     const uint32_t T = c->nt_pack, HM = c->crc_hmax;
     std::vector<uint16_t> pw((size_t)HM * T), pj(HM);
@@ -385,13 +394,13 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     const uint64_t F = c->max_frames;
     c->pcm_cap = F * (uint64_t)kBlock * c->C * c->B + 64;
     c->out_cap = F * (uint64_t)c->image_bytes;
-    if (hipMalloc(&c->d_crc_tab, 1024 * 2) || hipMalloc(&c->d_crc_pow, pw.size() * 2) ||
+    if (hipMalloc(&c->d_crc_tab, 2048 * 2) || hipMalloc(&c->d_crc_pow, pw.size() * 2) ||
         hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) || hipMalloc(&c->d_ctr, 16) ||
         hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_desc, F * (uint64_t)c->desc_stride) ||
         hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
         hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16) || hipMalloc(&c->d_stamps, 32 * 8))
         return fail(FLACGPU_ERR_OUT_OF_MEMORY);
-    if (hipMemcpy(c->d_crc_tab, tab.data(), 2048, hipMemcpyHostToDevice) ||
+    if (hipMemcpy(c->d_crc_tab, tab.data(), 4096, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_pow, pw.data(), pw.size() * 2, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_join, pj.data(), pj.size() * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) || hipMemset(c->d_ctr, 0, 16) ||
         hipMemset(c->d_stamps, 0, 32 * 8))

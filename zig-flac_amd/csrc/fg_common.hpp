@@ -104,6 +104,7 @@ struct EncodeArgs {
     uint32_t desc_stride;
     uint32_t image_bytes;       // pack kernel LDS frame-image bytes (multiple of 16, >= bound + 16)
     uint32_t stage_dbuf;        // full-frame analysis kernel: double-buffered staging (LDS-DMA prefetch)
+    uint32_t pack_dbuf;         // full-frame pack kernel: the same
     uint32_t *frame_bytes;      // [slot] exact frame bytes (analysis kernel)
     const uint64_t *offsets;    // [slot] byte offset of the frame in out (scan)
     uint8_t *out;               // contiguous output bitstream
@@ -111,7 +112,7 @@ struct EncodeArgs {
     uint32_t *work_ctr;         // 4 frame-queue tickets: analysis full/tail, pack full/tail (each
                                 // kernel zeroes the other stage's pair for its next launch)
     uint32_t *err;              // device error word (0 = ok; bit 0 invariant, bit 1 output too small)
-    const uint16_t *crc_tab;    // 4 x 256: z^40, z^32, z^24, z^16 byte tables (CRC-16/UMTS)
+    const uint16_t *crc_tab;    // 8 x 256: z^40, z^32, z^24, z^16, z^72, z^64, z^56, z^48 byte tables (CRC-16/UMTS)
     const uint16_t *crc_pow;    // [(H-1)*pack_threads + t] = z^(64*H*(T-1-t)) mod P, H = 1..crc_hmax
     const uint16_t *crc_join;   // [H-1] = z^(32*H)
     uint32_t crc_hmax;          // largest half-segment (words) of the CRC fold

@@ -191,6 +191,29 @@ __device__ __forceinline__ uint32_t crc_word(uint32_t crc, uint32_t W, const uin
 __device__ __forceinline__ uint32_t crc_byte(uint32_t crc, uint32_t b, const uint16_t *tab) {
     return ((crc << 8) & 0xFFFFu) ^ (uint32_t)tab[768 + (((crc >> 8) ^ b) & 255u)];
 }
+// Eight bytes per step (two stream words): only W0's bytes depend on the running CRC, so the
+// four lookups of W1 issue ahead of it.  tab[1024..2047] = z^72, z^64, z^56, z^48.
+__device__ __forceinline__ uint32_t crc_word2(uint32_t crc, uint32_t W0, uint32_t W1, const uint16_t *tab) {
+    const uint32_t X = W0 ^ (crc << 16);
+    return (uint32_t)tab[1024 + (X >> 24)] ^ (uint32_t)tab[1280 + ((X >> 16) & 255u)] ^
+           (uint32_t)tab[1536 + ((X >> 8) & 255u)] ^ (uint32_t)tab[1792 + (X & 255u)] ^ (uint32_t)tab[W1 >> 24] ^
+           (uint32_t)tab[256 + ((W1 >> 16) & 255u)] ^ (uint32_t)tab[512 + ((W1 >> 8) & 255u)] ^
+           (uint32_t)tab[768 + (W1 & 255u)];
+}
+// a(z) * b(z) mod P: the 31-bit carry-less product as a balanced XOR of 16 independent
+// terms (no serial bit loop), its top 15 bits folded back through the z^16 / z^24 tables.
+__device__ __forceinline__ uint32_t crc_mulmod_t(uint32_t a, uint32_t b, const uint16_t *tab) {
+    uint32_t t[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) t[i] = (b << i) & (uint32_t)(-(int32_t)((a >> i) & 1u));
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; i++) t[i] ^= t[i + w];
+    const uint32_t hi = t[0] >> 16;
+    return (t[0] & 0xFFFFu) ^ (uint32_t)tab[768 + (hi & 255u)] ^ (uint32_t)tab[512 + (hi >> 8)];
+}
+
 // a(z) * b(z) mod (z^16 + z^15 + z^2 + 1)
 __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
     uint32_t r = 0;
@@ -846,14 +869,21 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     // gridDim.x + (an atomic ticket) -- slower CUs (e.g. sharing SIMDs with the MD5 waves)
     // simply take fewer frames.  With double buffering the next frame's PCM is DMA'd into
     // the idle staging buffer while this one is analysed.
+    // The queue runs two frames ahead (as in k_pack): the job record of frame i+2 is loaded
+    // while frame i is analysed, so issuing frame i+1's DMA never waits on a global load.
     uint32_t *ctr = a.work_ctr + (FULL ? 0u : 1u);
     if (blockIdx.x == 0 && tid == 0) a.work_ctr[2] = a.work_ctr[3] = 0u;  // the pack kernel's queues
+    if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
+    __syncthreads();
     uint32_t jidx = blockIdx.x, buf = 0;
-    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, a.jobs[jidx].pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0);
+    uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
+    FrameJob job{}, jn{};
+    if (jidx < a.n_jobs) job = a.jobs[jidx];
+    if (nxt < a.n_jobs) jn = a.jobs[nxt];
+    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0);
     while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
         if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
-        const FrameJob job = a.jobs[jidx];
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.stage1 : LY.stage0));
 
@@ -861,10 +891,11 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         if (dbuf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
         __syncthreads();
-        const uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         if (dbuf && nxt < a.n_jobs)
-            stage_dma(a.pcm, a.jobs[nxt].pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave,
-                      NW, l);
+            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l);
+        FrameJob jnn{};
+        if (nn < a.n_jobs) jnn = a.jobs[nn];
         STAMP(0);
 
         // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
@@ -1500,12 +1531,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         }
         __syncthreads();  // params / records / scratch are reused by the next frame
         STAMP(6);
-        jidx = nxt;
+        jidx = nxt; job = jn; nxt = nn; jn = jnn;
         buf ^= 1u;
     }  // persistent frame loop
 #ifdef FG_STAMPS
-    if (l == 0 && a.stamps)
-        for (int i = 0; i < 7; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
+    if (l0 == 0 && a.stamps)
+        for (int i = 0; i < 8; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
 #endif
 }
 
@@ -1529,20 +1560,35 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
     const uint32_t C = NC ? (uint32_t)NC : a.channels;
     const uint32_t cw = 16u * C * B;
     const uint32_t cst = cw + stage_pad(C, B);
-    const PackLayout LY = pack_layout(C, B, a.image_bytes);
-    uint32_t *stg = (uint32_t *)(smem + LY.stage);
-    uint32_t *img = (uint32_t *)(smem + LY.img);
+    const bool dbuf = FULL && a.pack_dbuf != 0;
+    const PackLayout LY = pack_layout(C, B, a.image_bytes, dbuf);
     uint16_t *crct = (uint16_t *)(smem + LY.crc);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
-    for (uint32_t i = tid; i < 1024u; i += NT) crct[i] = a.crc_tab[i];
+    for (uint32_t i = tid; i < 2048u; i += NT) crct[i] = a.crc_tab[i];
     const bool stereo = a.stereo != 0;
 
+    // Persistent loop over a dynamic frame queue, two frames ahead: while frame i is packed, the
+    // PCM of frame i+1 arrives in the idle buffer by LDS-DMA and the job record of frame i+2 is
+    // loaded, so neither the staging nor the DMA issue waits on a global round trip.
     uint32_t *ctr = a.work_ctr + (FULL ? 2u : 3u);
     if (blockIdx.x == 0 && tid == 0) a.work_ctr[0] = a.work_ctr[1] = 0u;  // the analysis kernel's queues
-    for (uint32_t jidx = blockIdx.x, nxt = 0; jidx < a.n_jobs; jidx = nxt) {
+    if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
+    __syncthreads();
+    uint32_t jidx = blockIdx.x, buf = 0;
+    uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
+    FrameJob job{}, jn{};
+    if (jidx < a.n_jobs) job = a.jobs[jidx];
+    if (nxt < a.n_jobs) jn = a.jobs[nxt];
+    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, wave, NW, l0);
+#ifdef FG_STAMPS
+    uint64_t ph_[16] = {};
+    uint64_t tprev_ = __builtin_amdgcn_s_memtime();
+#endif
+    while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
         if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
-        const FrameJob job = a.jobs[jidx];
+        uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
+        uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
         const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
         const FrameDesc *F = (const FrameDesc *)fd;
@@ -1550,17 +1596,37 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         const uint32_t total_bits = F->total_bits;
         const uint32_t fbytes = ((total_bits + 7u) >> 3) + 2u;
         const uint64_t D = a.offsets[job.slot];
+        // CRC fold geometry and its shift constants, loaded early (used after the packing)
+        const uint32_t Lb = (total_bits + 7u) >> 3;
+        const uint32_t W4 = Lb >> 2;
+        const uint32_t H = ((W4 + 2u * NT - 1u) / (2u * NT)) | 1u;
+        const uint32_t hq = min(H, a.crc_hmax) - 1u;
+        const uint32_t crc_jw = a.crc_join[hq], crc_pw = a.crc_pow[hq * NT + tid];
         const bool skip = fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap;  // uniform
         const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
                        method = sd->method, cand = sd->cand;
+        // full frames: the Rice parameters of the lane's four 16-sample groups, loaded now so the
+        // packing never waits on a global read (partitions hold >= 16 samples: no group straddles)
+        uint32_t pq4[4] = {0, 0, 0, 0};
+        if constexpr (FULL) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) pq4[q] = sd->params[(l0 * 64u + 16u * q) >> (12u - o)];
+        }
 
-        // ---- 1. PCM -> LDS, candidate samples -> VGPRs
-        stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
+        // ---- 1. PCM -> LDS (already in flight with double buffering), candidate samples -> VGPRs
+        if (dbuf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
         __syncthreads();
-        nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        STAMP(0);
+        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        if (dbuf && nxt < a.n_jobs)
+            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, wave, NW, l);
+        FrameJob jnn{};
+        if (nn < a.n_jobs) jnn = a.jobs[nn];
         if (skip) {
             if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
             __syncthreads();
+            jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
             continue;
         }
         ST s[64];
@@ -1571,9 +1637,11 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         for (uint32_t t = 0; t < wave; t++) sub_start += ((const SubDesc *)(fd + sizeof(FrameDesc)) + t)->bits;
         const uint32_t lane_off = wave_incl_scan32(seg) - seg;
         __syncthreads();  // staging dead: zero the image
+        STAMP(1);
         const uint32_t Wz = (fbytes + 3u) / 4u + 2u;
         for (uint32_t i = tid; i < Wz; i += NT) img[i] = 0;
         __syncthreads();
+        STAMP(2);
         if (tid < 4) {
             const uint32_t hv = F->hdr[tid];
             if (hv) atomicOr(&img[tid], hv);
@@ -1602,6 +1670,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
             }
         }
 
+        STAMP(3);
         // ---- 3. pack: each lane writes its contiguous bit segment (frame_writer.zig:269-372).
         // Every field is ORed into the zeroed image at its bit position; the per-sample
         // code is branch-free (escape/rice/warm-up/partition header selected per lane).
@@ -1677,7 +1746,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
                     const uint32_t sh = 12u - o, psz = 4096u >> o;
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
-                        const uint32_t p = pp[(l * 64u + 16u * q) >> sh];
+                        const uint32_t p = pq4[q];
                         const uint32_t i0 = l * 64u + 16u * q;
                         part_header(p, i0 != 0 && (i0 & (psz - 1u)) == 0);
 #pragma unroll
@@ -1701,25 +1770,27 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         }
         __syncthreads();
 
+        STAMP(4);
         // ---- 4. CRC-16 of the frame: the word stream is front-padded with zero words (a no-op
         // for an init-0 CRC) to NT*2H words; thread t folds its 2H words as two interleaved
         // halves, joins them (x z^(32H)), shifts by z^(64H(NT-1-t)) and the workgroup
         // XOR-reduces.  H is odd so the per-thread word stride 2H costs at most 2-way conflicts.
-        const uint32_t Lb = (total_bits + 7u) >> 3;
-        const uint32_t W4 = Lb >> 2;
         {
-            uint32_t H = (W4 + 2u * NT - 1u) / (2u * NT);
-            H = H | 1u;
+            // two interleaved halves of H words per thread, eight bytes per step (H odd: one
+            // four-byte step at the end); words before the stream start read as zero
             const int32_t Z = (int32_t)(NT * 2u * H) - (int32_t)W4;
             uint32_t ca = 0, cb = 0;
             const int32_t va = (int32_t)(tid * 2u * H) - Z, vb = va + (int32_t)H;
-            for (uint32_t i = 0; i < H; i++) {
-                const int32_t ra = va + (int32_t)i, rb = vb + (int32_t)i;
-                if (ra >= 0) ca = crc_word(ca, img[ra], crct);
-                if (rb >= 0) cb = crc_word(cb, img[rb], crct);
+            auto word = [&](int32_t r) -> uint32_t { return r >= 0 ? img[r] : 0u; };
+            uint32_t i = 0;
+            for (; i + 1u < H; i += 2u) {
+                ca = crc_word2(ca, word(va + (int32_t)i), word(va + (int32_t)i + 1), crct);
+                cb = crc_word2(cb, word(vb + (int32_t)i), word(vb + (int32_t)i + 1), crct);
             }
-            const uint32_t ct = (ca ? crc_mulmod(ca, a.crc_join[H - 1u]) : 0u) ^ cb;
-            uint32_t contrib = ct ? crc_mulmod(ct, a.crc_pow[(H - 1u) * NT + tid]) : 0u;
+            ca = crc_word(ca, word(va + (int32_t)i), crct);
+            cb = crc_word(cb, word(vb + (int32_t)i), crct);
+            const uint32_t ct = crc_mulmod_t(ca, crc_jw, crct) ^ cb;
+            uint32_t contrib = crc_mulmod_t(ct, crc_pw, crct);
             contrib = wave_xor32(contrib);
             if (l == 0) misc[wave] = contrib;
         }
@@ -1733,6 +1804,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         }
         __syncthreads();
 
+        STAMP(5);
         // ---- 5. image -> out[D, D + fbytes): big-endian words realigned to the byte offset
         {
             const uint64_t E = D + fbytes;
@@ -1755,7 +1827,13 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
             }
         }
         __syncthreads();  // the image / staging area is reused by the next frame
+        STAMP(6);
+        jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
     }  // persistent frame loop
+#ifdef FG_STAMPS
+    if (l0 == 0 && a.stamps)
+        for (int i = 0; i < 7; i++) atomicAdd(&a.stamps[16 + i], (unsigned long long)ph_[i]);
+#endif
 }
 
 // persistent launch: grid = min(frames, resident workgroups)

@@ -23,9 +23,9 @@ struct AnaLayout {
 
 // Pack kernel (one wave per written subframe): staging, then the frame image.
 struct PackLayout {
-    uint32_t stage;  // PCM staging (aliases the image)
-    uint32_t img;    // frame image (big-endian 32-bit words)
-    uint32_t crc;    // 4 x 256 u16 CRC tables
+    uint32_t buf0;   // PCM staging of a frame, then (aliasing it) the frame image (big-endian words)
+    uint32_t buf1;   // second buffer: the next frame's PCM arrives by LDS-DMA (== buf0 without)
+    uint32_t crc;    // 8 x 256 u16 CRC tables
     uint32_t misc;   // 64 x u32 scratch (crc partials)
     uint32_t total;
 };
@@ -72,13 +72,15 @@ __host__ __device__ inline AnaLayout ana_layout(uint32_t C, uint32_t B, uint32_t
     return L;
 }
 
-__host__ __device__ inline PackLayout pack_layout(uint32_t C, uint32_t B, uint32_t image_bytes) {
+__host__ __device__ inline PackLayout pack_layout(uint32_t C, uint32_t B, uint32_t image_bytes, bool dbuf) {
     PackLayout L;
     uint32_t r0 = stage_bytes(C, B);
     if (image_bytes > r0) r0 = image_bytes;
-    L.stage = L.img = 0;
-    L.crc = fg_round16(r0);
-    L.misc = L.crc + 2048u;
+    r0 = fg_round16(r0);
+    L.buf0 = 0;
+    L.buf1 = dbuf ? r0 : 0u;
+    L.crc = dbuf ? 2u * r0 : r0;
+    L.misc = L.crc + 4096u;
     L.total = fg_round16(L.misc + 256u);
     return L;
 }
