@@ -173,8 +173,7 @@ __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16
 }
 
 // Full digest of n_streams independent byte ranges (offsets 4-byte aligned).
-// <= 64 VGPRs (8 waves/SIMD): the few MD5 waves must not crowd the encode waves off their SIMDs
-__global__ void __launch_bounds__(64, 6) k_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens,
+__global__ void __launch_bounds__(64) k_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens,
                                                     uint32_t n_streams, uint8_t *digests) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_streams) return;
