@@ -26,6 +26,7 @@ pytestmark = pytest.mark.gpu
     (3, 16, 48000, 9),
     (2, 8, 8000, 4),
     (1, 32, 48000, 12),
+    (7, 32, 96000, 12),   # the largest frame whose LPC tail kernel fits LDS
 ])
 def test_lpc_stream_parity(ch, bits, rate, q):
     check_stream(ch, bits, rate, 4096 * 66 + 1000, lpc_order=q)
@@ -70,3 +71,6 @@ def test_lpc_order_validation():
 
     with pytest.raises(flacgpu.FlacGpuError):
         flacgpu.Encoder(2, 16, 44100, lpc_order=13, max_frames=16)
+    # 8 channels x 32 bit with LPC: the tail kernel's LDS would exceed 160 KiB -> InvalidConfig
+    with pytest.raises(flacgpu.FlacGpuError):
+        flacgpu.Encoder(8, 32, 96000, lpc_order=8, max_frames=16)

@@ -25,6 +25,8 @@ CONFIGS = [
     (2, 8, 8000),
     (1, 24, 96000),
     (1, 32, 48000),
+    (8, 32, 192000),  # the largest frame the reference accepts: 8 x 4096 x 4 B
+    (7, 16, 44100),
 ]
 
 _encoders = {}

@@ -1061,8 +1061,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         uint64_t *psum = nullptr;
         uint32_t *pmax = nullptr;
         if constexpr (!FULL) {
-            psum = (uint64_t *)(smem + LY.psum) + wave * 512u;
-            pmax = (uint32_t *)(smem + LY.pmax) + wave * 512u;
+            psum = (uint64_t *)(smem + LY.psum) + wave * 256u;
+            pmax = (uint32_t *)(smem + LY.pmax) + wave * 256u;
         }
         // caps of rice.calcParams (rice.zig:97-103).  The while-clamp only changes the reference's
         // result where it would slice res[kw..ps] with ps < kw (UB there).  Full frames: n = 4096
@@ -1080,7 +1080,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         };
         auto zero_parts = [&]() {
             if constexpr (!FULL) {
-                for (uint32_t i = l; i < 512u; i += 64) {
+                for (uint32_t i = l; i < 256u; i += 64) {
                     psum[i] = 0;
                     pmax[i] = 0;
                 }
@@ -1183,8 +1183,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     }
                 }
             } else {
-                uint64_t *cs = psum, *ns = psum + 256;
-                uint32_t *cm = pmax, *nm = pmax + 256;
+                uint64_t *cs = psum;
+                uint32_t *cm = pmax;
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
                 for (int o = 8; o >= 0; o--) {
@@ -1203,13 +1203,17 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                         tots[o] = wave_sum32(cost);
                         fives[o] = (maxp > 14u && __any(five)) ? 1u : 0u;
                         if (o > 0) {
+                            // next coarser level in place: each pass reads entries 2j, 2j+1 (all
+                            // lanes, before any write of the pass) and writes entry j < 2j; later
+                            // passes read only entries above those written so far
                             for (uint32_t j = l; j < (np >> 1); j += 64) {
-                                ns[j] = cs[2 * j] + cs[2 * j + 1];
-                                nm[j] = cm[2 * j] | cm[2 * j + 1];
+                                const uint64_t s2 = cs[2 * j] + cs[2 * j + 1];
+                                const uint32_t m2 = cm[2 * j] | cm[2 * j + 1];
+                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                                cs[j] = s2;
+                                cm[j] = m2;
                             }
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                            uint64_t *ts = cs; cs = ns; ns = ts;
-                            uint32_t *tm = cm; cm = nm; nm = tm;
                         }
                     }
                 }

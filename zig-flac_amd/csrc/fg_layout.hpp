@@ -10,8 +10,8 @@ namespace fg {
 struct AnaLayout {
     uint32_t stage0; // PCM staging: 64 padded chunks
     uint32_t stage1; // second staging buffer (double-buffered LDS-DMA prefetch), or == stage0
-    uint32_t psum;   // tail kernel only: 2 x 256 u64 per wave
-    uint32_t pmax;   // tail kernel only: 2 x 256 u32 per wave
+    uint32_t psum;   // tail kernel only: 256 u64 per wave (levels combined in place)
+    uint32_t pmax;   // tail kernel only: 256 u32 per wave
     uint32_t par;    // rice params, 512 B per candidate wave (orders 0..8 at offset (1<<o)-1);
                      // with LPC two such buffers per wave (current best / candidate)
     uint32_t par_stride;
@@ -60,8 +60,8 @@ __host__ __device__ inline AnaLayout ana_layout(uint32_t C, uint32_t B, uint32_t
     }
     L.psum = L.pmax = end;
     if (!full) {
-        L.pmax = end + nw * 4096u;
-        end += nw * 6144u;
+        L.pmax = end + nw * 2048u;
+        end += nw * 3072u;
     }
     L.par = end;
     L.par_stride = lpc ? 1024u : 512u;
