@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--no-md5", action="store_true", help="skip the per-stream GPU MD5 (diagnostics only)")
     p.add_argument("--md5-join", action="store_true",
                    help="join each step's MD5 back into the encode stream (no overlap of consecutive steps)")
+    p.add_argument("--stream-pad", type=int, default=0,
+                   help="bytes of gap between consecutive streams in HBM (multiple of 4; layout diagnostics)")
     p.add_argument("--cpu-frames", type=int, default=32768, help="blocks in the CPU-baseline sample")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
@@ -94,11 +96,12 @@ def build_input(args, rank):
     rng = np.random.Generator(np.random.PCG64(20260821 + 7919 * rank))
     starts = rng.integers(0, (pool_n - n_per) // 4096 + 1, size=S) * 4096
     stream_bytes = n_per * fb
-    buf = np.empty(S * stream_bytes, dtype=np.uint8)
+    pitch = stream_bytes + args.stream_pad
+    buf = np.zeros(S * pitch, dtype=np.uint8)
     for s in range(S):
         a = int(starts[s]) * fb
-        buf[s * stream_bytes:(s + 1) * stream_bytes] = pcm_pool[a:a + stream_bytes]
-    offsets = [s * stream_bytes for s in range(S)]
+        buf[s * pitch:s * pitch + stream_bytes] = pcm_pool[a:a + stream_bytes]
+    offsets = [s * pitch for s in range(S)]
     samples = [n_per] * S
     return buf, offsets, samples
 

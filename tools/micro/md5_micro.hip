@@ -1,6 +1,7 @@
 // md5_micro.hip -- latency experiment for the per-stream MD5 (tools only).
 // Variants: 0 = one stream per lane (as k_md5_streams), 1 = two interleaved
-// streams per lane, 2 = rotate via shifts instead of v_alignbit.
+// streams per lane, 2 = rotate via shifts instead of v_alignbit, 3 = 16 active lanes,
+// 4 = H round as v_xad_u32 (3 dependent ops per step instead of 4).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
@@ -43,6 +44,30 @@ __device__ __forceinline__ void compress(uint32_t st[4], const uint32_t m[16]) {
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
 }
 
+__device__ __forceinline__ uint32_t xad(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm volatile("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ void compress_xad(uint32_t st[4], const uint32_t m[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t x, g;
+        if (i < 16) { g = i; x = ((b & c) | (~b & d)) + (a + K[i] + m[g]); }
+        else if (i < 32) { g = (5 * i + 1) & 15; x = ((d & b) | (~d & c)) + (a + K[i] + m[g]); }
+        else if (i < 48) { g = (3 * i + 5) & 15; x = xad(b, c ^ d, a + K[i] + m[g]); }
+        else { g = (7 * i) & 15; x = (c ^ (b | ~d)) + (a + K[i] + m[g]); }
+        const uint32_t t = d;
+        d = c;
+        c = b;
+        b = b + rotl<0>(x, S[i]);
+        a = t;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+}
+
 template <int V>
 __global__ void __launch_bounds__(64) k_md5(const uint32_t *data, uint64_t words_per_stream, uint32_t n, uint32_t *out) {
     const uint32_t s = blockIdx.x * 64 + threadIdx.x;
@@ -78,7 +103,7 @@ __global__ void __launch_bounds__(64) k_md5(const uint32_t *data, uint64_t words
         for (uint64_t b = 0; b < words_per_stream / 16; b++) {
             uint32_t m[16];
             for (int i = 0; i < 16; i++) m[i] = p[b * 16 + i];
-            compress<V == 2 ? 1 : 0>(st, m);
+            if (V == 4) compress_xad(st, m); else compress<V == 2 ? 1 : 0>(st, m);
         }
         out[s] = st[0] ^ st[1] ^ st[2] ^ st[3];
     }
@@ -94,7 +119,7 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    for (int v = 0; v < 4; v++) {
+    for (int v = 0; v < 5; v++) {
         for (int rep = 0; rep < 3; rep++) {
             hipEventRecord(e0);
             uint32_t grid = v == 3 ? n / 16 : (v == 1 ? n / 2 : n) / 64;
@@ -102,6 +127,7 @@ int main() {
             if (v == 1) hipLaunchKernelGGL(k_md5<1>, dim3(grid), dim3(64), 0, 0, d, words, n, o);
             if (v == 2) hipLaunchKernelGGL(k_md5<2>, dim3(grid), dim3(64), 0, 0, d, words, n, o);
             if (v == 3) hipLaunchKernelGGL(k_md5<3>, dim3(grid), dim3(64), 0, 0, d, words, n, o);
+            if (v == 4) hipLaunchKernelGGL(k_md5<4>, dim3(grid), dim3(64), 0, 0, d, words, n, o);
             hipEventRecord(e1);
             hipEventSynchronize(e1);
             float ms;

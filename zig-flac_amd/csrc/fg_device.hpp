@@ -959,10 +959,58 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         STAMP(2);
 
         uint32_t k = 0;
+        // Full 16-bit frames: bestOrder accumulates |e_q| per 16-sample group (the finest Rice
+        // partitions) for every order, so the chosen order's partition sums come out of it and
+        // the second residual pass only ORs zigzags (the escape widths).
+        constexpr bool FUSED = FULL && CLS == 16;
+        uint32_t tg[5][4];
         if (try_fixed) {
             // ---- 5. bestOrder (fixed.zig:85-167)
             uint64_t T[5];
-            if constexpr (CLS != 32) {
+            if constexpr (FUSED) {
+                const uint32_t KB = 0x7FFFFFFFu;
+                const uint32_t u1 = (uint32_t)h1, u2 = (uint32_t)h2, u3 = (uint32_t)h3, u4 = (uint32_t)h4;
+                uint32_t pb0 = u1 + KB;
+                uint32_t pb1 = (u1 - u2) + KB;
+                uint32_t pb2 = (u1 - 2u * u2 + u3) + KB;
+                uint32_t pb3 = (u1 - 3u * u2 + 3u * u3 - u4) + KB;
+#pragma unroll
+                for (int q = 0; q < 5; q++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++) tg[q][g] = 0;
+#pragma unroll
+                for (int j = 0; j < 64; j++) {
+                    const int g = j >> 4;
+                    const uint32_t b0 = (uint32_t)s[j] + KB;
+                    const uint32_t n0 = sad_u32(b0, KB, tg[0][g]);
+                    const uint32_t n1 = sad_u32(b0, pb0, tg[1][g]);
+                    const uint32_t b1 = (pb0 ^ KB) + b0;
+                    const uint32_t n2 = sad_u32(b1, pb1, tg[2][g]);
+                    const uint32_t b2 = (pb1 ^ KB) + b1;
+                    const uint32_t n3 = sad_u32(b2, pb2, tg[3][g]);
+                    const uint32_t b3 = (pb2 ^ KB) + b2;
+                    const uint32_t n4 = sad_u32(b3, pb3, tg[4][g]);
+                    if (j < 4) {  // lane 0: e_q[i] for i < q does not count (fixed.zig:102-127)
+                        const bool z = (l == 0);
+                        tg[0][g] = n0;
+                        tg[1][g] = !(z && j < 1) ? n1 : tg[1][g];
+                        tg[2][g] = !(z && j < 2) ? n2 : tg[2][g];
+                        tg[3][g] = !(z && j < 3) ? n3 : tg[3][g];
+                        tg[4][g] = !z ? n4 : tg[4][g];
+                    } else {
+                        tg[0][g] = n0; tg[1][g] = n1; tg[2][g] = n2; tg[3][g] = n3; tg[4][g] = n4;
+                    }
+                    pb0 = b0; pb1 = b1; pb2 = b2; pb3 = b3;
+                }
+                // per lane <= 64 * 2^21: row sums (16 lanes) stay below 2^32
+#define FG_ROWS64(v) ((uint64_t)rdl(v, 0) + rdl(v, 16) + rdl(v, 32) + rdl(v, 48))
+#pragma unroll
+                for (int q = 0; q < 5; q++) {
+                    const uint32_t r = row_sum32(tg[q][0] + tg[q][1] + tg[q][2] + tg[q][3]);
+                    T[q] = FG_ROWS64(r);
+                }
+#undef FG_ROWS64
+            } else if constexpr (CLS != 32) {
                 // biased differences b = e + 0x7FFFFFFF keep unsigned order == signed order:
                 // |e_{q+1}| = v_sad_u32(b_q, b_q[prev]) and b_{q+1} = (b_q[prev] ^ 0x7FFFFFFF) + b_q
                 const uint32_t KB = 0x7FFFFFFFu;
@@ -1243,7 +1291,13 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             const uint32_t P = part_cap(k);
             const uint32_t ps = n >> P;
             zero_parts();
-            {
+            if constexpr (FUSED) {
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    S8[g] = k == 0 ? tg[0][g] : k == 1 ? tg[1][g] : k == 2 ? tg[2][g] : k == 3 ? tg[3][g] : tg[4][g];
+                auto acc = [&](int j, bool warm, ST r) { O8[j >> 4] |= warm ? 0u : zigzag32((int32_t)r); };
+                FG_DISPATCH_K(k, (residuals_k<K, ST>(s, h1, h2, h3, h4, l, acc)))
+            } else {
                 auto acc = [&](int j, bool warm, ST r) { part_acc(S8, O8, ps, j, warm, (int32_t)r); };
                 FG_DISPATCH_K(k, (residuals_k<K, ST>(s, h1, h2, h3, h4, l, acc)))
             }
@@ -1747,7 +1801,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
                     pos += hl;
                 };
                 if constexpr (FULL) {
-                    const uint32_t sh = 12u - o, psz = 4096u >> o;
+                    const uint32_t psz = 4096u >> o;
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         const uint32_t p = pq4[q];

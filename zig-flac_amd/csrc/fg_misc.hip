@@ -134,9 +134,16 @@ constexpr uint32_t kMd5K[64] = {
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
 
 #define MD5_STEP(F, a, b, c, d, m, k, s) a = b + rotl(a + F(b, c, d) + (m) + (k), s)
+// H round: (b ^ (c ^ d)) + (a + m + k) as one v_xad_u32 whose other operands are off the
+// critical path -- 3 dependent ops per step instead of 4 (tools/micro/md5_micro.hip variant 4)
+__device__ __forceinline__ uint32_t xad_u32(uint32_t x, uint32_t y, uint32_t z) {
+    uint32_t r;
+    asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+    return r;
+}
+#define MD5_STEP_H(a, b, c, d, m, k, s) a = b + rotl(xad_u32(b, (c) ^ (d), a + (m) + (k)), s)
 #define MD5_F(b, c, d) (((b) & (c)) | (~(b) & (d)))
 #define MD5_G(b, c, d) (((b) & (d)) | ((c) & ~(d)))
-#define MD5_H(b, c, d) ((b) ^ (c) ^ (d))
 #define MD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
 
 __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16]) {
@@ -157,10 +164,10 @@ __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16
     }
 #pragma unroll
     for (int i = 32; i < 48; i += 4) {
-        MD5_STEP(MD5_H, a, b, c, d, m[(3 * i + 5) & 15], kMd5K[i + 0], 4);
-        MD5_STEP(MD5_H, d, a, b, c, m[(3 * i + 8) & 15], kMd5K[i + 1], 11);
-        MD5_STEP(MD5_H, c, d, a, b, m[(3 * i + 11) & 15], kMd5K[i + 2], 16);
-        MD5_STEP(MD5_H, b, c, d, a, m[(3 * i + 14) & 15], kMd5K[i + 3], 23);
+        MD5_STEP_H(a, b, c, d, m[(3 * i + 5) & 15], kMd5K[i + 0], 4);
+        MD5_STEP_H(d, a, b, c, m[(3 * i + 8) & 15], kMd5K[i + 1], 11);
+        MD5_STEP_H(c, d, a, b, m[(3 * i + 11) & 15], kMd5K[i + 2], 16);
+        MD5_STEP_H(b, c, d, a, m[(3 * i + 14) & 15], kMd5K[i + 3], 23);
     }
 #pragma unroll
     for (int i = 48; i < 64; i += 4) {
