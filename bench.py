@@ -5,13 +5,16 @@ metric : MSamples/s encoded (whole node), 44.1kHz/16-bit stereo, blocksize 4096
 unit   : 1 sample = one interchannel sample (STREAMINFO unit, metadata.zig:24)
 
 A "step" is one pass of the hot path over one batch: every 4096-sample block
-of S independent streams (32768 blocks per GPU by default, BASELINE config 2)
+of S independent streams (8192 streams x 8 blocks = 65536 blocks per GPU by
+default, BASELINE config 2)
 goes through the gfx950 kernels of libflacgpu.so -- analysis (mid/side, wasted
 bits, fixed-order analysis, Rice search, subframe choice, exact frame sizes),
 frame-size scan, pack (bit packing, CRC-8/16, frames written at their final
 offsets: one contiguous bitstream per stream) -- and the MD5 of every stream's
 raw PCM is computed on the GPU concurrently.  Inputs are resident in
-HBM before the timed region; outputs stay in HBM.
+HBM before the timed region; outputs stay in HBM.  The MD5 is sequential
+within a stream (one lane per stream), so its rate grows with the number of
+streams in flight: 8192 streams keep it under the encode.
 
 One process per GPU (torchrun for N > 1).  Streams are independent files, so
 ranks shard streams with no data-path collective (weak scaling); a barrier and
@@ -52,8 +55,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--frames", type=int, default=32768, help="4096-sample blocks per GPU")
-    p.add_argument("--streams", type=int, default=4096, help="independent streams (files) per GPU")
+    p.add_argument("--frames", type=int, default=65536, help="4096-sample blocks per GPU")
+    p.add_argument("--streams", type=int, default=8192, help="independent streams (files) per GPU")
     p.add_argument("--channels", type=int, default=2)
     p.add_argument("--bits", type=int, default=16)
     p.add_argument("--rate", type=int, default=44100)

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <cstdlib>
 
 constexpr uint32_t K[64] = {
     0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
@@ -109,8 +110,8 @@ __global__ void __launch_bounds__(64) k_md5(const uint32_t *data, uint64_t words
     }
 }
 
-int main() {
-    const uint32_t n = 4096;
+int main(int argc, char **argv) {
+    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 4096u;
     const uint64_t words = 128 * 1024 / 4;  // 128 KiB per stream
     uint32_t *d, *o;
     hipMalloc(&d, n * words * 4);

@@ -6,7 +6,7 @@
 # profiles/<tag>_summary.md + profiles/<tag>_pmc.json via tools/pmc_summary.py.
 set -e
 TAG=${1:-r1}; shift || true
-FRAMES=${1:-32768}; shift || true
+FRAMES=${1:-65536}; shift || true
 ARGS="--frames $FRAMES $@"
 REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
@@ -14,9 +14,9 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $REPO/bench.py --no-cpu $ARGS > $OUT/kt.log 2>&1
 i=0
-for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
+for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE" "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/pmc$i -o pmc -- python3 $REPO/bench.py --no-cpu $ARGS > $OUT/pmc$i.log 2>&1
+  timeout -s KILL 180 rocprofv3 --pmc $PMC --output-format csv -d $OUT/pmc$i -o pmc -- python3 $REPO/bench.py --no-cpu $ARGS > $OUT/pmc$i.log 2>&1 || { echo "PMC pass $i ($PMC) failed: no further GPU passes"; break; }
 done
 cd $REPO
 python3 tools/pmc_summary.py $OUT $TAG $FRAMES
