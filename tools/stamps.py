@@ -5,9 +5,10 @@ sys.path.insert(0, os.path.join(ROOT, "zig-flac_amd"))
 import numpy as np, torch
 import flacgpu, synth
 
-NAMES = ["stage wait", "sample load", "waste+eq", "bestOrder", "rice pass", "param search", "desc+rec+bar",
-         "stereo+exact"]
-PNAMES = ["stage+bar", "load+offsets", "zero img+bars", "residuals", "pack codes+bar", "CRC+bars", "store+bar"]
+NAMES = ["DMA issue+job load", "sample load", "waste+eq", "bestOrder", "rice pass", "param search", "desc+rec+bar",
+         "stereo+exact", "ticket atomic", "vmcnt(0) wait", "top barrier"]
+PNAMES = ["top barrier", "offsets+bar", "zero img+bars", "residuals", "pack codes+bar", "CRC+bars", "store+bar",
+          "ticket+desc loads", "vmcnt(0) wait", "DMA issue+sample load", "lane_bits/bits loads+scan"]
 S, F = 1024, 32
 enc = flacgpu.Encoder(2, 16, 44100, max_frames=S * F)
 L = enc.lib

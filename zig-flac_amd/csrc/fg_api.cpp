@@ -71,7 +71,9 @@ struct flacgpu_ctx {
     bool pack_dbuf = false;
     hipStream_t stream = nullptr, aux = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr, *d_crc_join = nullptr;
+    uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr, *d_crc_join = nullptr, *d_crc_pow4 = nullptr;
+    // full 16-bit two-channel frames are packed by k_pack4 (four waves per subframe): 512 threads
+    uint32_t nt_pack4 = 0, lds_pack4 = 0, crc_hmax4 = 0;
     uint32_t *d_err = nullptr, *d_ctr = nullptr;
     FrameJob *d_jobs = nullptr;
     uint8_t *d_desc = nullptr;
@@ -219,6 +221,8 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.work_ctr = c->d_ctr;
     a.crc_tab = c->d_crc_tab;
     a.crc_pow = c->d_crc_pow;
+    a.crc_pow4 = c->d_crc_pow4;
+    a.crc_hmax4 = c->crc_hmax4;
     a.crc_join = c->d_crc_join;
     a.crc_hmax = c->crc_hmax;
     a.records = c->records_on ? c->d_records : nullptr;
@@ -244,7 +248,8 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
         if (n_full) {
             a.jobs = d_jobs;
             a.n_jobs = (uint32_t)n_full;
-            HIPCHK(launch_stage(1, a, true, c->nt_pack, c->lds_pack, st));
+            if (c->nt_pack4) HIPCHK(launch_stage(1, a, true, c->nt_pack4, c->lds_pack4, st));
+            else HIPCHK(launch_stage(1, a, true, c->nt_pack, c->lds_pack, st));
         }
         if (n_tail) {
             a.jobs = d_jobs + n_full;
@@ -364,7 +369,16 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     c->lds_pack = pack_layout(c->C, c->B, c->image_bytes, c->pack_dbuf).total;
     // CRC fold: half-segments of H words (odd), H <= ceil(image words / (2 * pack threads))
     c->crc_hmax = ((c->image_bytes / 4u + 2u * c->nt_pack - 1u) / (2u * c->nt_pack)) | 1u;
-    if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u) {
+    if (c->C == 2 && c->B == 2 && !lpc) {
+        c->nt_pack4 = 512u;
+        if (const char *e = std::getenv("FLACGPU_PACK4")) c->nt_pack4 = e[0] == '0' ? 0u : 512u;  // A/B knob
+    }
+    if (c->nt_pack4) {
+        c->lds_pack4 = pack_layout(c->C, c->B, c->image_bytes, true).total;
+        c->crc_hmax4 = ((c->image_bytes / 4u + 2u * c->nt_pack4 - 1u) / (2u * c->nt_pack4)) | 1u;
+    }
+    if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u ||
+        c->lds_pack4 > 160u * 1024u) {
         delete c;
         return FLACGPU_ERR_INVALID_CONFIG;
     }
@@ -390,11 +404,16 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         pj[h - 1] = (uint16_t)crc_zpow(32ull * h);
         for (uint32_t t = 0; t < T; t++) pw[(size_t)(h - 1) * T + t] = (uint16_t)crc_zpow(64ull * h * (T - 1u - t));
     }
+    const uint32_t T4 = c->nt_pack4, HM4 = c->crc_hmax4;  // HM4 <= HM: pj covers both
+    std::vector<uint16_t> pw4((size_t)HM4 * T4 + 1);
+    for (uint32_t h = 1; h <= HM4; h++)
+        for (uint32_t t = 0; t < T4; t++) pw4[(size_t)(h - 1) * T4 + t] = (uint16_t)crc_zpow(64ull * h * (T4 - 1u - t));
 
     const uint64_t F = c->max_frames;
     c->pcm_cap = F * (uint64_t)kBlock * c->C * c->B + 64;
     c->out_cap = F * (uint64_t)c->image_bytes;
     if (hipMalloc(&c->d_crc_tab, 2048 * 2) || hipMalloc(&c->d_crc_pow, pw.size() * 2) ||
+        hipMalloc(&c->d_crc_pow4, pw4.size() * 2) ||
         hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) || hipMalloc(&c->d_ctr, 16) ||
         hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_desc, F * (uint64_t)c->desc_stride) ||
         hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
@@ -402,6 +421,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         return fail(FLACGPU_ERR_OUT_OF_MEMORY);
     if (hipMemcpy(c->d_crc_tab, tab.data(), 4096, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_pow, pw.data(), pw.size() * 2, hipMemcpyHostToDevice) ||
+        hipMemcpy(c->d_crc_pow4, pw4.data(), pw4.size() * 2, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_join, pj.data(), pj.size() * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) || hipMemset(c->d_ctr, 0, 16) ||
         hipMemset(c->d_stamps, 0, 32 * 8))
         return fail(FLACGPU_ERR_DEVICE);
@@ -418,6 +438,7 @@ void flacgpu_close(flacgpu_ctx *c) {
     for (auto e : c->event_pool) hipEventDestroy(e);
     hipFree(c->d_crc_tab);
     hipFree(c->d_crc_pow);
+    hipFree(c->d_crc_pow4);
     hipFree(c->d_crc_join);
     hipFree(c->d_err);
     hipFree(c->d_ctr);

@@ -116,6 +116,8 @@ struct EncodeArgs {
     const uint16_t *crc_pow;    // [(H-1)*pack_threads + t] = z^(64*H*(T-1-t)) mod P, H = 1..crc_hmax
     const uint16_t *crc_join;   // [H-1] = z^(32*H)
     uint32_t crc_hmax;          // largest half-segment (words) of the CRC fold
+    const uint16_t *crc_pow4;   // the same for the four-waves-per-subframe pack kernel (k_pack4, 512 threads)
+    uint32_t crc_hmax4;
     FrameRec *records;          // optional decision records [slot]
     unsigned long long *stamps; // diagnostic builds (-DFG_STAMPS): per-phase clock sums
 };

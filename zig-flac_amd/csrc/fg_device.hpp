@@ -14,10 +14,6 @@
 // fg_enc_b{1,2,3,4}.hip.
 #pragma once
 #include <hip/hip_runtime.h>
-#ifndef FG_NARROW
-#define FG_NARROW 0
-#endif
-
 #include <type_traits>
 
 #include "fg_common.hpp"
@@ -410,11 +406,20 @@ struct CandRes {
     } while (0)
 #endif
 
-// LDS-DMA one full frame into the padded staging area: each wave-instruction
-// moves <= 64 dwords of one 64-sample chunk (M0 = that chunk's LDS base).
+// LDS-DMA one full frame into the staging area.  Interleaved 16-bit stereo layout
+// (fg_layout.hpp): 16 instructions of 1 KiB, lane i of instruction k filling byte 16i of
+// block k from 16-B group i >> 2 of chunk 4k + (i & 3).  Padded layouts: each
+// wave-instruction moves <= 64 dwords of one 64-sample chunk (M0 = that chunk's base).
 __device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint32_t *stg, uint32_t cw, uint32_t cst,
-                                          uint32_t wave, uint32_t NW, uint32_t l) {
+                                          uint32_t wave, uint32_t NW, uint32_t l, bool ilv = false) {
     const uint32_t *src = (const uint32_t *)(pcm + off);
+    if (ilv) {
+        for (uint32_t k = wave; k < 16u; k += NW)
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void *)(src + (4u * k + (l & 3u)) * 64u + 4u * (l >> 2)),
+                (__attribute__((address_space(3))) void *)(stg + 272u * k), 16, 0, 0);
+        return;
+    }
     for (uint32_t ch = wave; ch < 64u; ch += NW) {
         for (uint32_t x0 = 0; x0 < cw; x0 += 64u) {
             if (x0 + l < cw)
@@ -429,7 +434,8 @@ __device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint
 // Stage one frame's interleaved PCM synchronously (tail frames zero-filled).
 template <bool FULL>
 __device__ __forceinline__ void stage_sync(const uint8_t *pcm, uint64_t off, uint32_t n, uint32_t CB, uint32_t *stg,
-                                           uint32_t cw, uint32_t cst, uint32_t wave, uint32_t NW, uint32_t l) {
+                                           uint32_t cw, uint32_t cst, uint32_t wave, uint32_t NW, uint32_t l,
+                                           bool ilv = false) {
     const uint32_t in_bytes = n * CB;
     const uint32_t *src = (const uint32_t *)(pcm + off);
     const uint32_t nchunks = FULL ? 64u : (n + 63u) >> 6;
@@ -443,7 +449,9 @@ __device__ __forceinline__ void stage_sync(const uint8_t *pcm, uint64_t off, uin
                 const uint8_t *sb = (const uint8_t *)src + 4u * wd;
                 for (uint32_t q = 0; 4u * wd + q < in_bytes; q++) v |= (uint32_t)sb[q] << (8 * q);
             }
-            stg[ch * cst + x] = v;
+            // interleaved 16-bit stereo layout: dword x of chunk ch at 272 (ch >> 2) + 16 (x >> 2) + 4 (ch & 3) + (x & 3)
+            if (ilv) stg[272u * (ch >> 2) + 16u * (x >> 2) + 4u * (ch & 3u) + (x & 3u)] = v;
+            else stg[ch * cst + x] = v;
         }
     }
 }
@@ -498,16 +506,16 @@ __device__ __forceinline__ void load_candidate(const uint32_t *stg, uint32_t cst
         const uint2 *p2 = (const uint2 *)lw;
         fill([&](int j, uint32_t c) -> int64_t { return (int32_t)(c ? p2[j].y : p2[j].x); },
              [&](int j) -> int64_t { return (int32_t)p2[j].y; });
-    } else if constexpr (NC == 2 && B == 2 && !FG_NARROW) {
-        // (L,R) packed in one dword per sample, read as explicit ds_read_b128 (the 16-B pad
-        // makes a quarter-wave's 16 lanes cover all 64 banks)
-        const uint4 *q4 = (const uint4 *)lw;
+    } else if constexpr (NC == 2 && B == 2) {
+        // (L,R) packed in one dword per sample, read as explicit ds_read_b128 from the
+        // interleaved layout (group t of this lane's chunk at 16 t dwords past its base)
+        const uint4 *q4 = (const uint4 *)(stg + 272u * (l >> 2) + 4u * (l & 3u));
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             uint32_t raw[16];
 #pragma unroll
             for (int t = 0; t < 4; t++) {
-                const uint4 v = q4[4 * g + t];
+                const uint4 v = q4[4 * (4 * g + t)];
                 raw[4 * t] = v.x; raw[4 * t + 1] = v.y; raw[4 * t + 2] = v.z; raw[4 * t + 3] = v.w;
             }
             auto put = [&](auto f) {
@@ -880,20 +888,23 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     FrameJob job{}, jn{};
     if (jidx < a.n_jobs) job = a.jobs[jidx];
     if (nxt < a.n_jobs) jn = a.jobs[nxt];
-    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0);
+    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0, NC == 2 && B == 2);
     while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
         if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
+        STAMP(8);
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.stage1 : LY.stage0));
 
         // ---- 1. the frame's interleaved PCM in LDS (64 padded chunks of 64 samples)
         if (dbuf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
+        else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+        STAMP(9);
         __syncthreads();
+        STAMP(10);
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         if (dbuf && nxt < a.n_jobs)
-            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l);
+            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l, NC == 2 && B == 2);
         FrameJob jnn{};
         if (nn < a.n_jobs) jnn = a.jobs[nn];
         STAMP(0);
@@ -1594,7 +1605,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     }  // persistent frame loop
 #ifdef FG_STAMPS
     if (l0 == 0 && a.stamps)
-        for (int i = 0; i < 8; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
+        for (int i = 0; i < 11; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
 #endif
 }
 
@@ -1637,7 +1648,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
     FrameJob job{}, jn{};
     if (jidx < a.n_jobs) job = a.jobs[jidx];
     if (nxt < a.n_jobs) jn = a.jobs[nxt];
-    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, wave, NW, l0);
+    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, wave, NW, l0, NC == 2 && B == 2);
 #ifdef FG_STAMPS
     uint64_t ph_[16] = {};
     uint64_t tprev_ = __builtin_amdgcn_s_memtime();
@@ -1672,13 +1683,15 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         }
 
         // ---- 1. PCM -> LDS (already in flight with double buffering), candidate samples -> VGPRs
+        STAMP(7);
         if (dbuf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l);
+        else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+        STAMP(8);
         __syncthreads();
         STAMP(0);
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         if (dbuf && nxt < a.n_jobs)
-            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, wave, NW, l);
+            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, wave, NW, l, NC == 2 && B == 2);
         FrameJob jnn{};
         if (nn < a.n_jobs) jnn = a.jobs[nn];
         if (skip) {
@@ -1689,11 +1702,13 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         }
         ST s[64];
         load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, s);  // (unused for CONSTANT)
+        STAMP(9);
         // lane offsets from the measured segment lengths (uniform prefix of earlier subframes)
         const uint32_t seg = sd->lane_bits[l];
         uint32_t sub_start = 8u * F->hdr_bytes;
         for (uint32_t t = 0; t < wave; t++) sub_start += ((const SubDesc *)(fd + sizeof(FrameDesc)) + t)->bits;
         const uint32_t lane_off = wave_incl_scan32(seg) - seg;
+        STAMP(10);
         __syncthreads();  // staging dead: zero the image
         STAMP(1);
         const uint32_t Wz = (fbytes + 3u) / 4u + 2u;
@@ -1890,9 +1905,11 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
     }  // persistent frame loop
 #ifdef FG_STAMPS
     if (l0 == 0 && a.stamps)
-        for (int i = 0; i < 7; i++) atomicAdd(&a.stamps[16 + i], (unsigned long long)ph_[i]);
+        for (int i = 0; i < 11; i++) atomicAdd(&a.stamps[16 + i], (unsigned long long)ph_[i]);
 #endif
 }
+
+#include "fg_pack4.hpp"
 
 // persistent launch: grid = min(frames, resident workgroups)
 template <typename KernelT>
@@ -1940,6 +1957,11 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
         return full ? launch_persistent(k_pack<B, CLS, true, MT, NCV, LPW>, a, threads, lds, st)         \
                     : launch_persistent(k_pack<B, CLS, false, MT, NCV, LPW>, a, threads, lds, st);       \
     } while (0)
+    if constexpr (B == 2 && CLS == 16 && LPW == 0) {
+        // full 16-bit two-channel frames: four waves per written subframe (fg_pack4.hpp)
+        if (stage == 1 && full && a.channels == 2 && threads == 512u)
+            return launch_persistent(k_pack4<512>, a, threads, lds, st);
+    }
     if (a.channels == 2) FG_L(2, 256);
     if (a.channels == 1) FG_L(1, 256);
     if (threads <= 256) FG_L(0, 256);

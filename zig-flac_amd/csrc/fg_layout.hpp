@@ -32,12 +32,17 @@ struct PackLayout {
 
 __host__ __device__ inline uint32_t fg_round16(uint32_t x) { return (x + 15u) & ~15u; }
 
-// Staging: 64 chunks (one per lane) of 16*C*B dwords plus a pad that makes the
-// per-lane reads bank-conflict free for the read width used: 16-bit stereo reads
-// ds_read_b128 (pad 4 dwords), 32-bit stereo ds_read_b64 (pad 2), the rest read
-// one sample at a time (pad 1).
+// Staging: 64 chunks (one per lane) of 16*C*B dwords.  16-bit stereo: blocks of 4
+// chunks, 1088 B apart, each block the 1 KiB destination of one 16-B LDS-DMA
+// instruction with the chunks' 16-B groups interleaved (group g of chunk 4b + c at
+// byte 64g + 16c of block b); lane l then reads group g at a per-lane base plus the
+// immediate 64g, and a quarter-wave's 16 ds_read_b128 cover all 64 banks (the 64-B
+// block pad staggers the four blocks).  Otherwise a pad makes the per-lane reads
+// conflict free: 32-bit stereo reads ds_read_b64 (pad 2 dwords), the rest one sample
+// at a time (pad 1).  Either way 64 * (16*C*B + pad) dwords.
+__host__ __device__ inline bool stage_ilv(uint32_t C, uint32_t B) { return C == 2 && B == 2; }
 __host__ __device__ inline uint32_t stage_pad(uint32_t C, uint32_t B) {
-    return (C == 2 && B == 2) ? 4u : ((C == 2 && B == 4) ? 2u : 1u);
+    return stage_ilv(C, B) ? 4u : ((C == 2 && B == 4) ? 2u : 1u);
 }
 __host__ __device__ inline uint32_t stage_bytes(uint32_t C, uint32_t B) {
     return 64u * (16u * C * B + stage_pad(C, B)) * 4u;

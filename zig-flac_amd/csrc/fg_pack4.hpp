@@ -1,0 +1,298 @@
+// fg_pack4.hpp -- frame packing for full 16-bit two-channel frames with four waves per
+// written subframe (included by fg_device.hpp inside namespace fg).
+//
+// The general pack kernel (k_pack) gives each written subframe one wave of 64-sample
+// lanes: 8 waves per CU, each lane emitting 64 codes in one dependent chain, so the
+// kernel is latency bound.  Here a lane owns 16 consecutive samples (wave 4s+q of the
+// workgroup packs quarter q of written subframe s), which gives 4x the waves and
+// 4x shorter chains.  Per frame (frame_writer.zig:269-372 restated):
+//   1. PCM arrives by 16-B LDS-DMA in a rotated layout: 16-sample chunk j holds its
+//      4-sample group g in 16-B slot (g + (j >> 2)) & 3, so the 16 lanes of a
+//      quarter-wave read 16 distinct bank groups (ds_read_b128, conflict free);
+//   2. each lane rebuilds its candidate samples (L, R, mid, side; encoder.zig:329-350)
+//      plus the 4 samples before them, applies the waste shift and the fixed-order
+//      residual (fixed.zig:30-76);
+//   3. code lengths (rice: (zz >> p) + 1 + p, escape: width; rice.zig / frame_writer.zig)
+//      -> a wave prefix scan on top of the quarter's base, which is the sum of the
+//      analysis kernel's exact 64-sample segment lengths before it;
+//   4. the codes are ORed into the zeroed LDS frame image, CRC-16 by the same
+//      front-padded parallel fold as k_pack, and the frame is stored at its final offset.
+#pragma once
+
+#ifndef FG_PACK4_MINW
+#define FG_PACK4_MINW 6
+#endif
+
+// Workgroup barrier for LDS hand-offs only: __syncthreads() would also wait for vmcnt(0),
+// i.e. drain the next frame's PCM DMA and this frame's output stores at every barrier.
+__device__ __forceinline__ void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// 16 instructions of 1 KiB: lane i of instruction k fills slot i & 3 of chunk 16k + (i >> 2)
+// from that chunk's 4-sample group ((i & 3) - (chunk >> 2)) & 3.
+__device__ __forceinline__ void stage_dma_rot(const uint8_t *pcm, uint64_t off, uint32_t *stg, uint32_t wave,
+                                              uint32_t NW, uint32_t l) {
+    const uint32_t *src = (const uint32_t *)(pcm + off);
+    for (uint32_t k = wave; k < 16u; k += NW) {
+        const uint32_t j = 16u * k + (l >> 2);
+        const uint32_t g = ((l & 3u) - (j >> 2)) & 3u;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + 16u * j + 4u * g),
+                                         (__attribute__((address_space(3))) void *)(stg + 256u * k), 16, 0, 0);
+    }
+}
+
+// dword offset of 4-sample group g of 16-sample chunk j in the rotated layout
+__device__ __forceinline__ uint32_t rot_off(uint32_t j, uint32_t g) { return 16u * j + 4u * ((g + (j >> 2)) & 3u); }
+
+template <int MAXT>
+__global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
+    constexpr uint32_t C = 2, B = 2;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+    const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l0 = lane_id();
+    const uint32_t sfi = wave >> 2, qw = wave & 3u;  // written subframe, quarter
+    const PackLayout LY = pack_layout(C, B, a.image_bytes, true);
+    uint16_t *crct = (uint16_t *)(smem + LY.crc);
+    uint32_t *misc = (uint32_t *)(smem + LY.misc);
+    for (uint32_t i = tid; i < 2048u; i += NT) crct[i] = a.crc_tab[i];
+    const bool stereo = a.stereo != 0;
+
+    uint32_t *ctr = a.work_ctr + 2u;
+    if (blockIdx.x == 0 && tid == 0) a.work_ctr[0] = a.work_ctr[1] = 0u;  // the analysis kernel's queues
+    if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
+    __syncthreads();
+    uint32_t jidx = blockIdx.x, buf = 0;
+    uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
+    FrameJob job{}, jn{};
+    if (jidx < a.n_jobs) job = a.jobs[jidx];
+    if (nxt < a.n_jobs) jn = a.jobs[nxt];
+    if (jidx < a.n_jobs) stage_dma_rot(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), wave, NW, l0);
+    while (jidx < a.n_jobs) {
+        const uint32_t l = opaque(l0);
+        if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
+        uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
+        uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
+        const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
+        const FrameDesc *F = (const FrameDesc *)fd;
+        const SubDesc *sd0 = (const SubDesc *)(fd + sizeof(FrameDesc));
+        const SubDesc *sd = sd0 + sfi;
+        const uint32_t total_bits = F->total_bits;
+        const uint32_t fbytes = ((total_bits + 7u) >> 3) + 2u;
+        const uint64_t D = a.offsets[job.slot];
+        const uint32_t Lb = (total_bits + 7u) >> 3;
+        const uint32_t W4 = Lb >> 2;
+        const uint32_t H = ((W4 + 2u * NT - 1u) / (2u * NT)) | 1u;
+        const uint32_t hq = min(H, a.crc_hmax4) - 1u;
+        const uint32_t crc_jw = a.crc_join[hq], crc_pw = a.crc_pow4[hq * NT + tid];
+        const bool skip = fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap;  // uniform
+        const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
+                       method = sd->method, cand = sd->cand;
+        const uint32_t i0 = 1024u * qw + 16u * l0;  // first sample of this lane
+        const uint32_t p = sd->params[i0 >> (12u - o)];
+        const uint32_t lb = sd->lane_bits[l0];
+        uint32_t sub_start = 8u * F->hdr_bytes;
+        if (sfi) sub_start += sd0->bits;
+
+        // ---- 1. PCM (DMA'd during the previous frame) -> this lane's samples and their history
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        if (nxt < a.n_jobs) stage_dma_rot(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), wave, NW, l);
+        FrameJob jnn{};
+        if (nn < a.n_jobs) jnn = a.jobs[nn];
+        if (skip) {
+            if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
+            __syncthreads();
+            jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= 1u;
+            continue;
+        }
+        const uint32_t j = 64u * qw + l;  // this lane's 16-sample chunk
+        uint32_t raw[20];                 // [0..3] the group before the chunk, [4..19] the chunk
+        {
+            const uint4 hv = j ? *(const uint4 *)(stg + rot_off(j - 1u, 3u)) : make_uint4(0, 0, 0, 0);
+            raw[0] = hv.x; raw[1] = hv.y; raw[2] = hv.z; raw[3] = hv.w;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint4 v = *(const uint4 *)(stg + rot_off(j, (uint32_t)g));
+                raw[4 + 4 * g] = v.x; raw[5 + 4 * g] = v.y; raw[6 + 4 * g] = v.z; raw[7 + 4 * g] = v.w;
+            }
+        }
+        // candidate samples (stereo: 0 L, 1 R, 2 mid, 3 side; otherwise channel `cand`)
+        const uint32_t kind = stereo ? cand : (cand ? 1u : 0u);
+        int32_t x[20];
+#pragma unroll
+        for (int i = 0; i < 20; i++) {
+            const int32_t L = (int32_t)(raw[i] << 16) >> 16, R = (int32_t)raw[i] >> 16;
+            x[i] = kind == 0 ? L : kind == 1 ? R : kind == 2 ? (L + R) >> 1 : L - R;
+        }
+        // lane offsets: quarter base = the analysis kernel's segment lengths before it
+        const uint32_t lbs = wave_incl_scan32(lb);
+        const uint32_t qbase = qw ? rdl(lbs, (int)(16u * qw - 1u)) : 0u;
+        bar_lds();  // staging dead: zero the image
+        const uint32_t Wz = (fbytes + 3u) / 4u + 2u;
+        for (uint32_t i = tid; i < Wz; i += NT) img[i] = 0;
+
+        // ---- 2. waste shift and residuals (fixed.zig:30-81), lengths of this lane's codes
+        const uint32_t bps = bd - w;
+        if (type != 0 && w != 0) {
+#pragma unroll
+            for (int i = 0; i < 20; i++) x[i] >>= w;
+        }
+        const bool first = (qw == 0) && (l == 0);
+        const uint32_t param_len = 4u + method;
+        const bool esc = (p & 0x80u) != 0;
+        const uint32_t wb = p & 0x7Fu, pr = esc ? 0u : p;
+        uint32_t r[16];
+        if (type == 2) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t u0 = (uint32_t)x[4 + i], u1 = (uint32_t)x[3 + i], u2 = (uint32_t)x[2 + i],
+                               u3 = (uint32_t)x[1 + i], u4 = (uint32_t)x[i];
+                uint32_t e;
+                if (k == 0) e = u0;
+                else if (k == 1) e = u0 - u1;
+                else if (k == 2) e = (u0 + u2) - 2u * u1;
+                else if (k == 3) e = (u0 - u3) + 3u * (u2 - u1);
+                else e = (u0 + u4) - 4u * (u1 + u3) + 6u * u2;
+                r[i] = e;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) r[i] = (uint32_t)x[4 + i];
+        }
+        // header bits (lane 0 of the subframe) and partition header bits (a lane opening a partition)
+        uint32_t len = 0;
+        if (first) {
+            if (type == 0) len = 8u + bd;
+            else if (type == 1) len = 8u + w;
+            else len = 8u + w + k * bps + 6u + param_len + (esc ? 5u : 0u);
+        } else if (type == 2 && (i0 & ((4096u >> o) - 1u)) == 0) {
+            len = param_len + (esc ? 5u : 0u);
+        }
+        if (type == 1) {
+            len += 16u * bps;
+        } else if (type == 2) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const bool warm = first && (uint32_t)i < k;
+                const uint32_t zz = zigzag32((int32_t)r[i]);
+                len = add_chain(len, warm ? 0u : (esc ? wb : (zz >> pr) + 1u + pr));
+            }
+        }
+        const uint32_t lane_off = wave_incl_scan32(len) - len;
+        bar_lds();  // image zeroed
+        if (tid < 4) {
+            const uint32_t hv = F->hdr[tid];
+            if (hv) atomicOr(&img[tid], hv);
+        }
+
+        // ---- 3. pack: each lane ORs its codes into the image at its bit offset
+        {
+            uint32_t pos = sub_start + qbase + lane_off;
+            const uint64_t mask = ~0ull >> (64 - (bps ? bps : 1u));
+            if (first) {
+                AtomicWriter bw;
+                bw.init(img, pos);
+                if (type == 0) {  // writeConstantSubframe: 0x00, value << waste in bd bits
+                    bw.put(0, 8);
+                    bw.put(((uint64_t)sd->cval << w) & (~0ull >> (64 - bd)), bd);
+                } else {
+                    const uint32_t tc = (type == 1) ? 1u : (8u | k);
+                    bw.put((tc << 1) | (w ? 1u : 0u), 8);
+                    if (w) bw.put(1, w);
+                    if (type == 2) {
+#pragma unroll
+                        for (int i = 0; i < 4; i++)  // warm-up samples
+                            if ((uint32_t)i < k) bw.put((uint64_t)(int64_t)x[4 + i] & mask, bps);
+                        bw.put((method << 4) | o, 6);
+                        if (esc) {
+                            bw.put(0x0Fu | (method << 4), 4u + method);
+                            bw.put(wb, 5);
+                        } else {
+                            bw.put(p, 4u + method);
+                        }
+                    }
+                }
+                pos = bw.pos;
+            } else if (type == 2 && (i0 & ((4096u >> o) - 1u)) == 0) {
+                const uint32_t esc_code = (0x0Fu | (method << 4)) << 5;
+                const uint32_t hl = param_len + (esc ? 5u : 0u);
+                put_or2(img, pos, esc ? (esc_code | wb) : p, hl);
+                pos += hl;
+            }
+            if (type == 1) {
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    put_or2(img, pos, (uint64_t)(int64_t)(int32_t)r[i] & mask, bps);
+                    pos += bps;
+                }
+            } else if (type == 2) {
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const bool warm = first && (uint32_t)i < k;
+                    const uint32_t zz = zigzag32((int32_t)r[i]);
+                    const uint32_t qz = (esc || warm) ? 0u : (zz >> pr);
+                    const uint64_t v = esc ? ((uint64_t)r[i] & (~0ull >> (64 - (wb ? wb : 1u))))
+                                           : (uint64_t)((1u << pr) | (zz & ((1u << pr) - 1u)));
+                    const uint32_t cl = warm ? 0u : (esc ? wb : pr + 1u);
+                    pos += qz;
+                    put_or2(img, pos, v, cl);
+                    pos += cl;
+                }
+            }
+        }
+        bar_lds();
+
+        // ---- 4. CRC-16 of the frame (front-padded parallel fold, as k_pack)
+        {
+            const int32_t Z = (int32_t)(NT * 2u * H) - (int32_t)W4;
+            uint32_t ca = 0, cb = 0;
+            const int32_t va = (int32_t)(tid * 2u * H) - Z, vb = va + (int32_t)H;
+            auto word = [&](int32_t rr) -> uint32_t { return rr >= 0 ? img[rr] : 0u; };
+            uint32_t i = 0;
+            for (; i + 1u < H; i += 2u) {
+                ca = crc_word2(ca, word(va + (int32_t)i), word(va + (int32_t)i + 1), crct);
+                cb = crc_word2(cb, word(vb + (int32_t)i), word(vb + (int32_t)i + 1), crct);
+            }
+            ca = crc_word(ca, word(va + (int32_t)i), crct);
+            cb = crc_word(cb, word(vb + (int32_t)i), crct);
+            const uint32_t ct = crc_mulmod_t(ca, crc_jw, crct) ^ cb;
+            uint32_t contrib = crc_mulmod_t(ct, crc_pw, crct);
+            contrib = wave_xor32(contrib);
+            if (l == 0) misc[wave] = contrib;
+        }
+        bar_lds();
+        if (tid == 0) {
+            uint32_t crc = 0;
+            for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
+            for (uint32_t b = W4 * 4u; b < Lb; b++)
+                crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+            put_bits(img, Lb * 8u, crc, 16);
+        }
+        bar_lds();
+
+        // ---- 5. image -> out[D, D + fbytes): big-endian words realigned to the byte offset
+        {
+            const uint64_t E = D + fbytes;
+            const uint64_t q0 = D >> 2, q1 = (E + 3u) >> 2;
+            const uint32_t sa = (uint32_t)(D & 3u);
+            uint32_t *o32 = (uint32_t *)a.out;
+            for (uint64_t q = q0 + tid; q < q1; q += NT) {
+                const uint32_t m = (uint32_t)(q - q0);
+                const uint32_t lo = img[m];
+                const uint32_t hi = m ? img[m - 1u] : 0u;
+                const uint32_t v = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(hi, lo, sa) : lo);
+                const uint64_t b0 = 4u * q;
+                if (b0 >= D && b0 + 4u <= E) {
+                    o32[q] = v;
+                } else {
+#pragma unroll
+                    for (uint32_t b = 0; b < 4; b++)
+                        if (b0 + b >= D && b0 + b < E) a.out[b0 + b] = (uint8_t)(v >> (8 * b));
+                }
+            }
+        }
+        bar_lds();  // the image / staging area is reused by the next frame (its reads are done)
+        jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= 1u;
+    }  // persistent frame loop
+}
