@@ -20,7 +20,7 @@
 #pragma once
 
 #ifndef FG_PACK4_MINW
-#define FG_PACK4_MINW 6
+#define FG_PACK4_MINW 8
 #endif
 
 // Workgroup barrier for LDS hand-offs only: __syncthreads() would also wait for vmcnt(0),
