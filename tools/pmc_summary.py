@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 FAMILIES = [("analyze_tail", r"k_analyze<\d+, \d+, false"), ("analyze", r"k_analyze<\d+, \d+, true"),
-            ("pack_tail", r"k_pack<\d+, \d+, false"), ("pack", r"k_pack<\d+, \d+, true"),
+            ("pack_tail", r"k_pack<\d+, \d+, false"), ("pack", r"k_pack<\d+, \d+, true"), ("pack", r"k_pack4<"),
             ("scan", r"k_scan"), ("md5", r"k_md5_streams"), ("md5_blocks", r"k_md5_blocks")]
 
 
@@ -60,7 +60,7 @@ def main():
     json.dump(out, open(os.path.join(root, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
     lines = [f"# rocprofv3 summary: {tag}", "", f"frames per launch: {frames}", "",
              "| kernel | calls | avg us | % time | HBM MB/launch (corrected) |", "|---|---|---|---|---|"]
-    for fam in [f for f, _ in FAMILIES if f in stats]:
+    for fam in dict.fromkeys(f for f, _ in FAMILIES if f in stats):
         s = stats[fam]
         h = hbm.get(fam)
         lines.append(f"| {fam} | {s['calls']} | {s['avg_ns']/1e3:.1f} | {s['pct']:.1f} | "
