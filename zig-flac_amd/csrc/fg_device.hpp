@@ -176,6 +176,34 @@ __device__ __forceinline__ uint32_t rice_choose(uint64_t S, uint32_t len, uint32
     return 0x80u | width;
 }
 
+// The same decision for a partition sum known to fit 32 bits (16-bit input, partitions of
+// <= 2048 samples: |e| <= 2^20).  Every intermediate then fits 32 bits: f(p) uses
+// S >> (p-1) <= 2*len unless p was clamped to maxp-1 >= 13, where S >> 13 < 2^19.
+__device__ __forceinline__ uint32_t rice_choose(uint32_t S, uint32_t len, uint32_t width, uint32_t maxp,
+                                                uint32_t *cost) {
+    uint32_t p;
+    if (S <= ((len + 1u) >> 1)) {
+        p = 0;
+    } else {
+        const uint32_t two = 2u * len;
+        uint32_t m = 0;
+        if (S > two) {
+            m = bitlen32(S) - bitlen32(two);
+            if ((S >> m) > two) m++;
+        }
+        p = m + 1u;
+    }
+    if (p > maxp - 1u) p = maxp - 1u;
+    const uint32_t f = (p == 0) ? len + (S << 1) : (1u + p) * len + ((S >> (p - 1u)) - (len >> 1));
+    const uint32_t esc = (width <= 31u) ? 5u + width * len : ~0u;
+    if (f < esc) {
+        *cost = f;
+        return p;
+    }
+    *cost = esc;
+    return 0x80u | width;
+}
+
 // CRC-16/UMTS helpers (crc16.zig; poly 0x8005, init 0).  tab = 4 x 256 u16:
 // [0] x*z^40, [1] x*z^32, [2] x*z^24, [3] x*z^16 (mod P).  W is a stream word
 // whose first byte sits in bits 31..24.
@@ -1170,24 +1198,37 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 uint32_t W8[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) W8[q] = bitlen32(O8[q]);
-                const uint64_t S7a = (uint64_t)S8[0] + S8[1], S7b = (uint64_t)S8[2] + S8[3];
+                // 16-bit fixed prediction: every partition below order 0 sums < 2^32 (|e| <= 2^20)
+                using SW = typename std::conditional<(CLS == 16 && LPW == 0), uint32_t, uint64_t>::type;
+                const SW S7a = (SW)S8[0] + (SW)S8[1], S7b = (SW)S8[2] + (SW)S8[3];
                 const uint32_t W7a = max(W8[0], W8[1]), W7b = max(W8[2], W8[3]);
-                const uint64_t S6 = S7a + S7b;
+                const SW S6 = S7a + S7b;
                 const uint32_t W6 = max(W7a, W7b);
                 // levels 5..2: partitions of 2/4/8/16 lanes -> DPP butterflies (every lane of the
                 // group ends up with the group value); levels 1, 0: the four row values (uniform)
-                uint64_t Sl[4];
+                SW Sl[4];
                 uint32_t Wl[4];
                 {
-                    uint64_t Sg = S6;
+                    SW Sg = S6;
                     uint32_t Wg = W6;
-                    Sg += dpp64<DPP_XOR1>(Sg); Wg = max(Wg, dpp<DPP_XOR1>(Wg)); Sl[0] = Sg; Wl[0] = Wg;
-                    Sg += dpp64<DPP_XOR2>(Sg); Wg = max(Wg, dpp<DPP_XOR2>(Wg)); Sl[1] = Sg; Wl[1] = Wg;
-                    Sg += dpp64<DPP_HMIRROR>(Sg); Wg = max(Wg, dpp<DPP_HMIRROR>(Wg)); Sl[2] = Sg; Wl[2] = Wg;
-                    Sg += dpp64<DPP_MIRROR>(Sg); Wg = max(Wg, dpp<DPP_MIRROR>(Wg)); Sl[3] = Sg; Wl[3] = Wg;
+                    if constexpr (sizeof(SW) == 4) {
+                        Sg += dpp<DPP_XOR1>(Sg); Wg = max(Wg, dpp<DPP_XOR1>(Wg)); Sl[0] = Sg; Wl[0] = Wg;
+                        Sg += dpp<DPP_XOR2>(Sg); Wg = max(Wg, dpp<DPP_XOR2>(Wg)); Sl[1] = Sg; Wl[1] = Wg;
+                        Sg += dpp<DPP_HMIRROR>(Sg); Wg = max(Wg, dpp<DPP_HMIRROR>(Wg)); Sl[2] = Sg; Wl[2] = Wg;
+                        Sg += dpp<DPP_MIRROR>(Sg); Wg = max(Wg, dpp<DPP_MIRROR>(Wg)); Sl[3] = Sg; Wl[3] = Wg;
+                    } else {
+                        Sg += dpp64<DPP_XOR1>(Sg); Wg = max(Wg, dpp<DPP_XOR1>(Wg)); Sl[0] = Sg; Wl[0] = Wg;
+                        Sg += dpp64<DPP_XOR2>(Sg); Wg = max(Wg, dpp<DPP_XOR2>(Wg)); Sl[1] = Sg; Wl[1] = Wg;
+                        Sg += dpp64<DPP_HMIRROR>(Sg); Wg = max(Wg, dpp<DPP_HMIRROR>(Wg)); Sl[2] = Sg; Wl[2] = Wg;
+                        Sg += dpp64<DPP_MIRROR>(Sg); Wg = max(Wg, dpp<DPP_MIRROR>(Wg)); Sl[3] = Sg; Wl[3] = Wg;
+                    }
                 }
-                const uint64_t r0 = rdl64(Sl[3], 0), r1 = rdl64(Sl[3], 16), r2 = rdl64(Sl[3], 32),
-                               r3 = rdl64(Sl[3], 48);
+                uint64_t r0, r1, r2, r3;  // row sums (uniform); order 0 may reach 2^32
+                if constexpr (sizeof(SW) == 4) {
+                    r0 = rdl(Sl[3], 0); r1 = rdl(Sl[3], 16); r2 = rdl(Sl[3], 32); r3 = rdl(Sl[3], 48);
+                } else {
+                    r0 = rdl64(Sl[3], 0); r1 = rdl64(Sl[3], 16); r2 = rdl64(Sl[3], 32); r3 = rdl64(Sl[3], 48);
+                }
                 const uint32_t m0 = rdl(Wl[3], 0), m1 = rdl(Wl[3], 16), m2 = rdl(Wl[3], 32), m3 = rdl(Wl[3], 48);
 #pragma unroll
                 for (int o = 0; o < 9; o++) {
@@ -1198,7 +1239,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                             const int per = 1 << (o - 6);
 #pragma unroll
                             for (int q = 0; q < per; q++) {
-                                uint64_t S;
+                                SW S;
                                 uint32_t W;
                                 if (o == 8) { S = S8[q]; W = W8[q]; }
                                 else if (o == 7) { S = q ? S7b : S7a; W = q ? W7b : W7a; }
@@ -1485,19 +1526,23 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     uint32_t pq[4];
 #pragma unroll
                     for (int q = 0; q < 4; q++) pq[q] = pp[(l * 64u + 16u * q) >> sh];
-                    uint32_t sg[2] = {seg, 0u};  // two interleaved chains
+                    // per 16-sample group (one Rice parameter each): sum of the quotients only;
+                    // the unary stop bits and low bits (cnt * (1 + p)), an escape group's
+                    // cnt * width and the partition headers are added once per group
+                    uint32_t qa[4] = {0u, 0u, 0u, 0u};
                     auto len_a = [&](int j, bool warm, ST r) {
-                        const uint32_t p = pq[j >> 4];
-                        const bool esc = (p & 0x80u) != 0;
-                        const uint32_t i = l * 64u + j;
-                        if ((j & 15) == 0 && i != 0 && (i & (psz - 1u)) == 0)
-                            sg[1] = add_chain(sg[1], param_len + (esc ? 5u : 0u));
                         const uint32_t zz = zigzag32((int32_t)r);
-                        const uint32_t cl = esc ? (p & 0x7Fu) : (zz >> p) + 1u + p;
-                        sg[j & 1] = add_chain(sg[j & 1], warm ? 0u : cl);
+                        qa[j >> 4] = add_chain(qa[j >> 4], warm ? 0u : (zz >> (pq[j >> 4] & 31u)));
                     };
                     pass(len_a);
-                    seg = sg[0] + sg[1];
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        const uint32_t p = pq[g], i = l * 64u + 16u * g;
+                        const bool esc = (p & 0x80u) != 0;
+                        const uint32_t cnt = 16u - ((g == 0 && l == 0) ? k : 0u);  // warm-ups: lane 0, j < k
+                        seg += esc ? cnt * (p & 0x7Fu) : qa[g] + cnt * (1u + p);
+                        if (i != 0 && (i & (psz - 1u)) == 0) seg += param_len + (esc ? 5u : 0u);
+                    }
                 } else {
                     const uint32_t psz = n >> o;
                     auto len_a = [&](int j, bool warm, ST r) {
