@@ -183,3 +183,22 @@ def test_write_frame_planar():
         got = enc.write_frame(np.stack(planes), f)
         ref, _ = oracle_ref.encode_frame(planes, n, f, ch, bits, rate)
         assert got == ref, (f, n, _diff_msg(got, ref))
+
+
+@pytest.mark.parametrize("stereo", [True, False])
+def test_pack4_matches_general_pack(monkeypatch, stereo):
+    """Full 16-bit two-channel frames go through k_pack4 (four waves per subframe); the
+    general one-wave-per-subframe k_pack (FLACGPU_PACK4=0) must emit the same bytes."""
+    import flacgpu
+
+    n = 4096 * 48 + 77  # full frames (incl. the special blocks) and a short tail
+    pcm = synth.synth_pcm(n, 2, 16, 44100, stream=5)
+    outs = []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("FLACGPU_PACK4", knob)
+        with flacgpu.Encoder(2, 16, 44100, max_frames=64, stereo_decorrelation=stereo) as enc:
+            outs.append(enc.encode_frames(pcm))
+    assert outs[0][1] == outs[1][1], "frame sizes differ between k_pack4 and k_pack"
+    assert outs[0][0] == outs[1][0], _diff_msg(outs[0][0], outs[1][0])
+    ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, 2, 16, 44100, stereo=stereo)
+    assert outs[0][0] == ref, _diff_msg(outs[0][0], ref)

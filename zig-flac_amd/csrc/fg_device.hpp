@@ -983,8 +983,21 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             if constexpr (CLS != 32) x0 = (ST)rdl((uint32_t)s[0], 0);
             else x0 = (ST)rdl64((uint64_t)s[0], 0);
             bool eq = true;
+            if constexpr (CLS != 32) {
+                // all equal to x0 <=> max == min == x0: v_max3/v_min3 over the samples instead of a
+                // compare per sample feeding a serial scalar AND chain (samples past n count as x0)
+                int32_t mx = (int32_t)x0, mn = (int32_t)x0;
 #pragma unroll
-            for (int j = 0; j < 64; j++) eq &= (s[j] == x0) || (!FULL && l * 64u + j >= n);
+                for (int j = 0; j < 64; j++) {
+                    const int32_t v = (!FULL && l * 64u + j >= n) ? (int32_t)x0 : (int32_t)s[j];
+                    mx = max(mx, v);
+                    mn = min(mn, v);
+                }
+                eq = (mx == (int32_t)x0) && (mn == (int32_t)x0);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 64; j++) eq &= (s[j] == x0) || (!FULL && l * 64u + j >= n);
+            }
             if (__all(eq)) {
                 R.type = 0;
                 R.est = bps;
