@@ -202,3 +202,29 @@ def test_pack4_matches_general_pack(monkeypatch, stereo):
     assert outs[0][0] == outs[1][0], _diff_msg(outs[0][0], outs[1][0])
     ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, 2, 16, 44100, stereo=stereo)
     assert outs[0][0] == ref, _diff_msg(outs[0][0], ref)
+
+
+@pytest.mark.parametrize("cfg,max_frames,n", [
+    ((2, 16, 44100), 8, 4096 * 37 + 1001),   # 4-frame chunks: 10 chunks, both halves reused 5x, a tail
+    ((2, 24, 96000), 6, 4096 * 13),          # 3-frame chunks, no tail
+    ((1, 16, 44100), 2, 4096 * 5 + 3),       # 1-frame chunks
+])
+def test_host_pipeline_matches_sequential(cfg, max_frames, n):
+    """flacgpu_encode_frames overlaps chunk i+1's upload and encode with chunk i's download
+    (two halves of the context's buffers, a download thread) once an input spans more than
+    one chunk; bytes and frame sizes must equal a single-chunk encode and the oracle."""
+    import flacgpu
+
+    ch, bits, rate = cfg
+    pcm = synth.synth_pcm(n, ch, bits, rate, stream=11)
+    with flacgpu.Encoder(ch, bits, rate, max_frames=max_frames) as enc:
+        got, sizes = enc.encode_frames(pcm, first_frame=3)
+        again, sizes2 = enc.encode_frames(pcm, first_frame=3)  # context reuse: halves and events recycled
+    with flacgpu.Encoder(ch, bits, rate, max_frames=1024) as enc:
+        seq, seq_sizes = enc.encode_frames(pcm, first_frame=3)
+    assert sizes == seq_sizes and sizes2 == seq_sizes
+    assert got == seq, _diff_msg(got, seq)
+    assert again == seq
+    ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, ch, bits, rate, first_frame=3)
+    assert sizes == ref_sizes
+    assert got == ref, _diff_msg(got, ref)

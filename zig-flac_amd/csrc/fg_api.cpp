@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/flacgpu.h"
@@ -70,6 +71,7 @@ struct flacgpu_ctx {
     bool stage_dbuf = false;
     bool pack_dbuf = false;
     hipStream_t stream = nullptr, aux = nullptr;
+    hipStream_t dl = nullptr;  // download stream of the pipelined host-buffer path
     hipEvent_t fork = nullptr, join = nullptr;
     uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr, *d_crc_join = nullptr, *d_crc_pow4 = nullptr;
     // full 16-bit two-channel frames are packed by k_pack4 (four waves per subframe): 512 threads
@@ -389,6 +391,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     };
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    if (hipStreamCreateWithFlags(&c->dl, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
 
@@ -456,8 +459,103 @@ void flacgpu_close(flacgpu_ctx *c) {
     if (c->fork) hipEventDestroy(c->fork);
     if (c->join) hipEventDestroy(c->join);
     if (c->aux) hipStreamDestroy(c->aux);
+    if (c->dl) hipStreamDestroy(c->dl);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
+}
+
+// Host buffers in, host buffers out, with the PCIe directions overlapped: the context's
+// device buffers split into two halves, chunk i+1 is uploaded and encoded on c->stream
+// while a worker thread downloads chunk i's frames on c->dl (pageable copies block the
+// issuing thread, so the two directions need two threads).  Output bytes and frame sizes
+// are identical to the sequential loop; only the schedule differs.
+static int encode_frames_pipelined(flacgpu_ctx *c, const uint8_t *src, uint64_t n_samples, uint64_t first_frame_number,
+                                   uint8_t *out, size_t out_cap, size_t *out_len, uint32_t *frame_bytes) {
+    const uint32_t bs = c->cfg.block_size;
+    const uint64_t stride = (uint64_t)bs * c->C * c->B;
+    const uint64_t total_frames = frames_for(n_samples, bs);
+    // chunks of at most 2048 frames (32 MiB of 16-bit stereo) so that long inputs keep both
+    // PCIe directions busy; the halves of the context's buffers hold one chunk each
+    const uint64_t F = std::min<uint64_t>(c->max_frames / 2u, 2048u);
+    const uint64_t pcm_half = (uint64_t)(c->max_frames / 2u) * kBlock * c->C * c->B;  // 16-B multiple
+    const uint64_t out_half = (uint64_t)(c->max_frames / 2u) * c->image_bytes;
+    const uint64_t fb_half = c->max_frames / 2u;
+    hipEvent_t done[2] = {get_event(c), get_event(c)};
+    if (!done[0] || !done[1]) return FLACGPU_ERR_DEVICE;
+    size_t written = 0;
+    int wrc = FLACGPU_OK;  // the worker's result
+    std::thread worker;
+    auto download = [&](int set, uint64_t frame0, uint64_t nf) {
+        wrc = FLACGPU_OK;
+        if (hipSetDevice(c->device) != hipSuccess || hipEventSynchronize(done[set]) != hipSuccess) {
+            wrc = FLACGPU_ERR_DEVICE;
+            return;
+        }
+        uint64_t total = 0;
+        if (hipMemcpyAsync(&total, c->d_total + set, 8, hipMemcpyDeviceToHost, c->dl) != hipSuccess ||
+            hipStreamSynchronize(c->dl) != hipSuccess) {
+            wrc = FLACGPU_ERR_DEVICE;
+            return;
+        }
+        if (written + total > out_cap) {
+            wrc = FLACGPU_ERR_OUTPUT_TOO_SMALL;
+            return;
+        }
+        if ((frame_bytes && hipMemcpyAsync(frame_bytes + frame0, c->d_fbytes + set * fb_half, nf * 4, hipMemcpyDeviceToHost,
+                                           c->dl) != hipSuccess) ||
+            hipMemcpyAsync(out + written, c->d_out + set * out_half, total, hipMemcpyDeviceToHost, c->dl) != hipSuccess ||
+            hipStreamSynchronize(c->dl) != hipSuccess) {
+            wrc = FLACGPU_ERR_DEVICE;
+            return;
+        }
+        written += total;
+    };
+    int rc = FLACGPU_OK;
+    uint64_t frame0 = 0;
+    for (int set = 0; frame0 < total_frames && rc == FLACGPU_OK; set ^= 1) {
+        const uint64_t nf = std::min<uint64_t>(F, total_frames - frame0);
+        const uint64_t s0 = frame0 * bs;
+        const uint64_t ns = std::min<uint64_t>(nf * bs, n_samples - s0);
+        uint8_t *dp = c->d_pcm + set * pcm_half;
+        // chunk i - 1's download (worker) overlaps this upload; chunk i - 2 used this half
+        if (hipMemcpyAsync(dp, src + s0 * c->C * c->B, ns * c->C * c->B, hipMemcpyHostToDevice, c->stream) !=
+            hipSuccess) {
+            rc = FLACGPU_ERR_DEVICE;
+            break;
+        }
+        if (launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, first_frame_number + frame0, (uint32_t)nf,
+                             c->stream) != hipSuccess) {
+            rc = FLACGPU_ERR_DEVICE;
+            break;
+        }
+        const uint64_t n_full = (bs == (uint32_t)kBlock) ? ns / kBlock : 0;
+        if ((rc = encode_core(c, dp, c->d_jobs, n_full, nf - n_full, c->d_desc, c->d_fbytes + set * fb_half,
+                              c->d_out + set * out_half, out_half, c->d_offsets, c->d_total + set, c->stream)))
+            break;
+        if (hipEventRecord(done[set], c->stream) != hipSuccess) {
+            rc = FLACGPU_ERR_DEVICE;
+            break;
+        }
+        // chunk i - 1's download ran beside this chunk's upload and encode (the other half);
+        // it must end before the next worker (output order) and before half set ^ 1 is reused
+        if (worker.joinable()) {
+            worker.join();
+            if ((rc = wrc)) break;
+        }
+        worker = std::thread(download, set, frame0, nf);
+        frame0 += nf;
+    }
+    if (worker.joinable()) {
+        worker.join();
+        if (rc == FLACGPU_OK) rc = wrc;
+    }
+    hipStreamSynchronize(c->stream);
+    c->event_pool.push_back(done[0]);
+    c->event_pool.push_back(done[1]);
+    if (rc) return rc;
+    if ((rc = check_device_error(c))) return rc;
+    *out_len = written;
+    return FLACGPU_OK;
 }
 
 int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
@@ -477,6 +575,12 @@ int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sa
     uint64_t frame0 = 0;
     size_t written = 0;
     if (c->records_on) c->h_records.clear();
+    if (!c->records_on && c->max_frames >= 2 && total_frames > std::min<uint64_t>(c->max_frames / 2u, 2048u)) {
+        const int rc = encode_frames_pipelined(c, src, n_samples, first_frame_number, out, out_cap, out_len,
+                                               frame_bytes);
+        resolve_timing(c);
+        return rc;
+    }
     while (frame0 < total_frames) {
         const uint64_t nf = std::min<uint64_t>(c->max_frames, total_frames - frame0);
         const uint64_t s0 = frame0 * bs;
