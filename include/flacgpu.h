@@ -91,6 +91,22 @@ int flacgpu_encode_frames(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_
                           uint64_t first_frame_number, uint8_t *out, size_t out_cap, size_t *out_len,
                           uint32_t *frame_bytes);
 
+/* ---- Multi-GPU host-buffer encode (SURVEY.md §8(b) "flacgpu_open_multi") --
+ * One process, n_devices contexts (device ordinals may repeat).  A call shards
+ * the input's frames into contiguous ranges, one per context, encodes them
+ * concurrently (one host thread per context, each with its own PCIe link) and
+ * concatenates the frames in frame order into out -- the bitstream
+ * concatenation step of the multi-rank path, done in host memory because the
+ * caller's output already lives there.  Same arguments, errors and output as
+ * flacgpu_encode_frames (byte-identical to one context encoding it all). */
+typedef struct flacgpu_multi flacgpu_multi;
+int flacgpu_open_multi(int n_devices, const int *devices, const flacgpu_config *cfg, uint32_t max_frames_per_call,
+                       flacgpu_multi **out);
+void flacgpu_close_multi(flacgpu_multi *m);
+int flacgpu_multi_encode_frames(flacgpu_multi *m, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
+                                uint64_t first_frame_number, uint8_t *out, size_t out_cap, size_t *out_len,
+                                uint32_t *frame_bytes);
+
 /* Encoder.writeFrame for one frame, exactly the reference call: the caller
  * provides planar i32 samples (the reference's Encoder.samples[ch][0..n],
  * encoder.zig:23, each within bits_per_sample signed range), the frame number

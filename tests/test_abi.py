@@ -83,3 +83,22 @@ def test_fails_loudly_without_device():
 def test_strerror():
     lib = flacgpu.load_library()
     assert lib.flacgpu_strerror(-5).decode().startswith("HIP device error")
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-device failure path")
+def test_multi_fails_loudly_without_device():
+    with pytest.raises(flacgpu.FlacGpuError) as e:
+        flacgpu.MultiEncoder([0, 0], 2, 16, 44100)
+    assert e.value.code == -5
+
+
+def test_multi_rejects_bad_arguments():
+    lib = flacgpu.load_library()
+    cfg = lib.flacgpu_config_default(2, 16, 44100)
+    h = ctypes.c_void_p()
+    devs = (ctypes.c_int * 1)(0)
+    assert lib.flacgpu_open_multi(0, devs, ctypes.byref(cfg), 16, ctypes.byref(h)) == -2 and not h.value
+    assert lib.flacgpu_open_multi(1, None, ctypes.byref(cfg), 16, ctypes.byref(h)) == -2 and not h.value
+    n = ctypes.c_size_t(0)
+    assert lib.flacgpu_multi_encode_frames(None, None, 2, 0, 0, None, 0, ctypes.byref(n), None) == -2
+    lib.flacgpu_close_multi(None)  # no-op

@@ -228,3 +228,22 @@ def test_host_pipeline_matches_sequential(cfg, max_frames, n):
     ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, ch, bits, rate, first_frame=3)
     assert sizes == ref_sizes
     assert got == ref, _diff_msg(got, ref)
+
+
+@pytest.mark.parametrize("devices,n", [
+    ([0, 0], 4096 * 21 + 77),     # two contexts on one GPU: 11 + 11 frames, ragged tail in the second
+    ([0, 0, 0], 4096 * 2 + 5),    # more contexts than frames: one shard is empty
+    ([0], 4096 * 9),
+])
+def test_multi_encode_matches_single(devices, n):
+    """flacgpu_multi_encode_frames shards contiguous frame ranges over contexts (one per GPU in
+    production; repeated ordinals here, on the one-GPU box) and concatenates them in frame
+    order: the bytes and frame sizes equal one context's and the oracle's."""
+    import flacgpu
+
+    pcm = synth.synth_pcm(n, 2, 16, 44100, stream=13)
+    with flacgpu.MultiEncoder(devices, 2, 16, 44100, max_frames=8) as me:
+        got, sizes = me.encode_frames(pcm, first_frame=200)
+    ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, 2, 16, 44100, first_frame=200)
+    assert sizes == ref_sizes
+    assert got == ref, _diff_msg(got, ref)

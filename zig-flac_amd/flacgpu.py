@@ -192,6 +192,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_vorbis_comment_bytes": (SZ, [I32, P]),
         "flacgpu_encode_file": (I32, [P, P, U32, U64, P, SZ, ctypes.POINTER(SZ)]),
         "flacgpu_wav_to_flac": (I32, [I32, P, SZ, P, SZ, ctypes.POINTER(SZ)]),
+        "flacgpu_open_multi": (I32, [I32, P, ctypes.POINTER(Config), U32, ctypes.POINTER(P)]),
+        "flacgpu_close_multi": (None, [P]),
+        "flacgpu_multi_encode_frames": (I32, [P, P, U32, U64, U64, P, SZ, ctypes.POINTER(SZ), P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -212,7 +215,7 @@ def exported_symbols() -> list:
         "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_get_records",
         "flacgpu_get_config", "flacgpu_wav_parse", "flacgpu_streaminfo_init", "flacgpu_streaminfo_update_frame_size",
         "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file",
-        "flacgpu_wav_to_flac",
+        "flacgpu_wav_to_flac", "flacgpu_open_multi", "flacgpu_close_multi", "flacgpu_multi_encode_frames",
     ]
 
 
@@ -392,3 +395,43 @@ class Encoder:
         arr = (FrameRecord * max(n.value, 1))()
         _check(self.lib.flacgpu_get_records(self.ctx, arr, n.value, ctypes.byref(n)), "get_records")
         return list(arr)[: n.value]
+
+
+class MultiEncoder:
+    """One input's frames sharded over several GPUs of this process (flacgpu_open_multi):
+    contiguous frame ranges encoded concurrently, concatenated in frame order."""
+
+    def __init__(self, devices: Sequence[int], channels: int, bits: int, sample_rate: int, max_frames: int = 32768,
+                 block_size: int = 4096):
+        self.lib = load_library()
+        self.cfg = Config(sample_rate, block_size, channels, bits, 1, 8, 30, 0)
+        self.channels, self.bytes_per_sample, self.block_size = channels, bits // 8, block_size
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        _check(self.lib.flacgpu_open_multi(len(devices), devs, ctypes.byref(self.cfg), max_frames, ctypes.byref(h)),
+               "open_multi")
+        self.m = h
+
+    def close(self) -> None:
+        if getattr(self, "m", None):
+            self.lib.flacgpu_close_multi(self.m)
+            self.m = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def encode_frames(self, pcm: bytes, first_frame: int = 0):
+        per = self.channels * self.bytes_per_sample
+        n = len(pcm) // per
+        nf = (n + self.block_size - 1) // self.block_size
+        cap = nf * self.lib.flacgpu_frame_bound_bytes(ctypes.byref(self.cfg)) + 64
+        out = ctypes.create_string_buffer(cap)
+        sizes = (ctypes.c_uint32 * max(nf, 1))()
+        out_len = ctypes.c_size_t(0)
+        src = ctypes.create_string_buffer(bytes(pcm), len(pcm)) if pcm else None
+        _check(self.lib.flacgpu_multi_encode_frames(self.m, src, self.bytes_per_sample, n, first_frame, out, cap,
+                                                    ctypes.byref(out_len), sizes), "multi_encode_frames")
+        return out.raw[: out_len.value], list(sizes)[:nf]
