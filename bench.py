@@ -177,6 +177,29 @@ def read_traffic(kernel, frames_per_launch):
         return None
 
 
+def read_issue(kernel, frames_per_launch, avg_s):
+    """VALU issue load of `kernel` from the committed PMC summary: wave-instructions per launch
+    against 1024 SIMDs x 0.5 wave64 VALU instructions/clock (SIMD-32, 2 passes; MI355X_MICROARCH.md)
+    at 2.4 GHz.  A lower bound on VALU busy (64-bit and transcendental ops take more passes)."""
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    if not cands or avg_s <= 0:
+        return None
+    try:
+        d = json.load(open(cands[-1]))
+        if d.get("frames_per_launch") != frames_per_launch:
+            return None
+        c = d.get("counters_per_dispatch", {}).get(kernel, {})
+        valu, salu = c.get("SQ_INSTS_VALU"), c.get("SQ_INSTS_SALU")
+        if not valu:
+            return None
+        peak = 1024 * 0.5 * 2.4e9
+        return {"valu_wave_instr_per_launch": valu, "salu_wave_instr_per_launch": salu,
+                "peak_valu_wave_instr_per_s": peak, "valu_issue_frac": round(valu / avg_s / peak, 4),
+                "source": os.path.basename(cands[-1])}
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -332,6 +355,7 @@ def main():
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "launches": n_launch,
                 "encode_path_gbs": round(path_bytes / path_s / 1e9, 2) if path_s > 0 else None,
+                "issue": read_issue(dom, n_frames, avg_s),
             },
             "kernel_ms_per_step": {k: round(v[1] / max(v[0], 1), 4) for k, v in kt.items() if v[0]},
             "output_ok": ok,
