@@ -919,7 +919,6 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0, NC == 2 && B == 2);
     while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
-        if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
         STAMP(8);
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.stage1 : LY.stage0));
@@ -930,11 +929,13 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         STAMP(9);
         __syncthreads();
         STAMP(10);
-        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         if (dbuf && nxt < a.n_jobs)
             stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l, NC == 2 && B == 2);
-        FrameJob jnn{};
-        if (nn < a.n_jobs) jnn = a.jobs[nn];
+        // The ticket of the frame after next is taken here, behind this frame's wait for its
+        // staged PCM, and its value is first used at the estimate barrier (step 9): taken at the
+        // top of the loop, the vmcnt(0) for the DMA also waited for the atomic's round trip.
+        uint32_t tk = 0;
+        if (tid == 0) tk = atomicAdd(ctr, 1u);
         STAMP(0);
 
         // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
@@ -1454,7 +1455,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             uint32_t *rc = recs + cand * 16u;
             rc[6] = (uint32_t)R.est; rc[7] = (uint32_t)(R.est >> 32);
         }
+        if (tid == 0) misc[20] = gridDim.x + tk;
         __syncthreads();
+        // the job record of the frame after next (DMA'd at the top of the next frame)
+        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        FrameJob jnn{};
+        if (nn < a.n_jobs) jnn = a.jobs[nn];
         uint32_t channel_code, n_out;
         int my_slot;
         if (stereo) {
