@@ -1662,7 +1662,11 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 fr->pad = 0;
             }
         }
-        __syncthreads();  // params / records / scratch are reused by the next frame
+        // params / records / scratch are reused by the next frame: with double-buffered staging
+        // nothing touches LDS between here and the next frame's top barrier, which then orders
+        // this frame's last reads before the next frame's writes; synchronous staging writes the
+        // staging buffer before that barrier, so it needs its own
+        if (!dbuf) __syncthreads();
         STAMP(6);
         jidx = nxt; job = jn; nxt = nn; jn = jnn;
         buf ^= 1u;
