@@ -292,7 +292,8 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
                 }
             }
         }
-        bar_lds();  // the image / staging area is reused by the next frame (its reads are done)
+        // no barrier here: the image / staging area is next written by the DMA issued after the
+        // next frame's top barrier, which already orders this frame's last reads before it
         jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= 1u;
     }  // persistent frame loop
 }
