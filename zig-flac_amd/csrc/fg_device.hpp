@@ -1967,7 +1967,10 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
                 }
             }
         }
-        __syncthreads();  // the image / staging area is reused by the next frame
+        // the image / staging area is reused by the next frame: with double buffering it is next
+        // written by the DMA issued after the next frame's top barrier, which orders these reads
+        // before it; synchronous staging refills it before that barrier
+        if (!dbuf) __syncthreads();
         STAMP(6);
         jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
     }  // persistent frame loop
