@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FLACGPU_ABI_VERSION 2
+#define FLACGPU_ABI_VERSION 3
 
 /* Error codes (map to the Zig error set
  * {OutOfMemory, WriteFailed, DeviceError, InvalidConfig, InvalidInput}). */
@@ -116,7 +116,15 @@ int flacgpu_encode_frame_planar(flacgpu_ctx *ctx, const int32_t *const planes[8]
                                 uint64_t frame_number, uint8_t *out, size_t out_cap, uint32_t *frame_bytes);
 
 /* ---- Streaming MD5 (md5.zig, fed by wav_reader.zig:66; finalised by
- *      Encoder.finalizeStreamInfoMd5, encoder.zig:168-170) on the GPU ------- */
+ *      Encoder.finalizeStreamInfoMd5, encoder.zig:168-170) -------------------
+ * One stream's MD5 is a strictly sequential chain.  The default engine hashes
+ * on a host core (about 10x one GPU lane's rate, and the bytes are already in
+ * host memory on this path); FLACGPU_MD5_DEVICE runs the chain on one GPU
+ * lane (opt-in; the device-resident plans below hash many streams at once, one
+ * lane per stream).  set_engine resets the running hash. */
+enum { FLACGPU_MD5_HOST = 0, FLACGPU_MD5_DEVICE = 1 };
+int flacgpu_md5_set_engine(flacgpu_ctx *ctx, int engine);
+int flacgpu_md5_get_engine(const flacgpu_ctx *ctx);
 int flacgpu_md5_init(flacgpu_ctx *ctx);
 int flacgpu_md5_update(flacgpu_ctx *ctx, const void *data, size_t len);
 int flacgpu_md5_final(flacgpu_ctx *ctx, uint8_t digest[16]);
@@ -137,6 +145,32 @@ uint64_t flacgpu_plan_frames(const flacgpu_plan *plan);
 uint64_t flacgpu_plan_out_bound(const flacgpu_plan *plan);
 /* First frame index of stream s inside the plan's frame table. */
 uint64_t flacgpu_plan_stream_first_frame(const flacgpu_plan *plan, uint32_t s);
+
+/* A plan whose streams are SEGMENTS of longer streams (a stream spans several
+ * batches, as the reference's block loop spans a whole file, wav2flac.zig:66-97):
+ * stream s's frames are numbered from first_frame_numbers[s] (NULL: 0) and
+ * final_segment[s] == 0 marks a segment the stream continues after (NULL: every
+ * segment final).  A non-final segment must hold whole frames of block_size
+ * samples and a whole number of 64-byte MD5 blocks (always true at 4096). */
+int flacgpu_plan_create_segments(flacgpu_ctx *ctx, uint32_t n_streams, const uint64_t *stream_offsets,
+                                 const uint64_t *stream_samples, uint32_t bytes_per_sample,
+                                 const uint64_t *first_frame_numbers, const uint8_t *final_segment,
+                                 flacgpu_plan **out);
+/* Move every frame number of the plan on by `frames`, queued on hip_stream: the
+ * next window of the same streams at the same device offsets (a ring buffer the
+ * caller refills).  Frame numbers stay u36. */
+int flacgpu_plan_advance(flacgpu_plan *plan, uint64_t frames, void *hip_stream);
+
+/* Per-stream MD5 chaining state carried from one call to the next (device
+ * memory, 32 bytes per stream; initialise with flacgpu_md5_state_init and copy
+ * to the device). */
+typedef struct {
+    uint32_t h[4];      /* MD5 chaining value */
+    uint64_t bytes;     /* message bytes absorbed */
+    uint32_t finished;  /* 1 once the final segment has been padded */
+    uint32_t reserved;
+} flacgpu_md5_state;
+void flacgpu_md5_state_init(flacgpu_md5_state *states, size_t n);
 
 /* Encode every frame of the plan from device PCM d_pcm into the contiguous
  * device buffer d_out (capacity out_cap).  Per frame: d_frame_bytes[f] (u32)
@@ -161,6 +195,24 @@ int flacgpu_encode_plan_device_md5_async(flacgpu_ctx *ctx, const flacgpu_plan *p
                                          uint8_t *d_out, uint64_t out_cap, uint32_t *d_frame_bytes,
                                          uint64_t *d_frame_offsets, uint64_t *d_total, uint8_t *d_md5,
                                          void *hip_stream, void *md5_stream);
+
+/* flacgpu_encode_plan_device with carried MD5 state: if d_md5_state is non-NULL,
+ * each stream's state is read, advanced by its segment and written back (the
+ * MD5 of a stream spanning many calls); segments marked final are padded and
+ * their digest written to d_md5[16 s] (if non-NULL).  With d_md5_state NULL every
+ * segment must be final (fresh state, digest to d_md5).  md5_stream as in
+ * flacgpu_encode_plan_device_md5_async (NULL: joined into hip_stream). */
+int flacgpu_encode_plan_device_ex(flacgpu_ctx *ctx, const flacgpu_plan *plan, const void *d_pcm, uint8_t *d_out,
+                                  uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets,
+                                  uint64_t *d_total, flacgpu_md5_state *d_md5_state, uint8_t *d_md5,
+                                  void *hip_stream, void *md5_stream);
+
+/* Synchronise hip_stream (NULL: the context's stream) and report the device-side
+ * error word of the kernels queued so far (FLACGPU_ERR_OUTPUT_TOO_SMALL when a
+ * frame would not fit out_cap, FLACGPU_ERR_INTERNAL on a violated invariant);
+ * clears it.  The device-resident entry points are asynchronous: this is how
+ * their caller learns of a failure. */
+int flacgpu_sync_check(flacgpu_ctx *ctx, void *hip_stream);
 
 /* ---- File level (host code around the GPU frame path) --------------------- */
 
@@ -208,7 +260,9 @@ size_t flacgpu_vorbis_comment_bytes(int last_metadata, uint8_t out[31]);
 
 /* wav2flac (wav2flac.zig:10-97) for PCM in memory: the 73-byte header (STREAMINFO not
  * last, VORBIS_COMMENT last) + every frame, STREAMINFO carrying the frame-size
- * min/max and the MD5 of the PCM bytes (both computed on the GPU). */
+ * min/max (from the GPU's per-frame sizes, replayed in frame order) and the MD5 of
+ * the PCM bytes (the context's MD5 engine; the host engine hashes on a thread
+ * that runs beside the GPU encode). */
 int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
                         uint8_t *out, size_t out_cap, size_t *out_len);
 /* The whole conversion of an in-memory WAV file on HIP device `device`

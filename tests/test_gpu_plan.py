@@ -1,0 +1,238 @@
+"""The device-resident plan path -- the path bench.py times -- against the CPU
+restatement, byte for byte.
+
+flacgpu_plan_create[_segments] + flacgpu_encode_plan_device[_md5_async|_ex]
+over many independent streams in one device PCM buffer: every stream's
+bitstream, per-frame sizes and MD5 digest are compared with
+oracle_ref.encode_stream / hashlib on the same PCM (the reference's per-file
+block loop, wav2flac.zig:66-97, with the MD5 of wav_reader.zig:66 finalised as
+in encoder.zig:168-170).  Covers ragged lengths (0 and 1 sample, tails,
+multiples of 4096), stream offsets at every 4-byte alignment mod 16, plans
+larger than the context (plan-owned descriptors), both MD5 schedules, streams
+spanning several calls with carried MD5 state, frame-number windows
+(flacgpu_plan_advance), and the device error word (flacgpu_sync_check).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle_ref
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    return torch, torch.device("cuda", 0)
+
+
+def _layout(lengths, fb, aligns, gap=36):
+    """Byte offsets for streams of `lengths` interchannel samples; offset % 16 cycles through aligns."""
+    offs, pos = [], 0
+    for i, n in enumerate(lengths):
+        want = aligns[i % len(aligns)]
+        pos += (want - pos) % 16
+        offs.append(pos)
+        pos += n * fb + gap
+        pos = (pos + 3) & ~3
+    return offs, pos + 64
+
+
+def _run_plan(enc, pcm_all, offs, lengths, md5="join", first_frames=None, final=None, states=None, out_cap=None,
+              advance=0):
+    import flacgpu
+
+    torch, dev = _torch()
+    plan = enc.plan(offs, lengths, first_frames=first_frames, final=final)
+    d_pcm = torch.from_numpy(np.frombuffer(pcm_all, dtype=np.uint8).copy()).to(dev)
+    cap = int(plan.out_bound) if out_cap is None else out_cap
+    d_out = torch.zeros(max(int(plan.out_bound), 1), dtype=torch.uint8, device=dev)
+    nfr = max(int(plan.n_frames), 1)
+    d_fb = torch.zeros(nfr, dtype=torch.int32, device=dev)
+    d_off = torch.zeros(nfr, dtype=torch.int64, device=dev)
+    d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
+    d_md5 = torch.zeros(max(len(offs), 1) * 16, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev)
+    if advance:
+        plan.advance(advance, st.cuda_stream)
+    if md5 == "state":
+        d_state = states if states is not None else torch.from_numpy(
+            np.frombuffer(flacgpu.md5_states(len(offs)), dtype=np.uint8).copy()).to(dev)
+        enc.encode_plan_device_ex(plan, d_pcm.data_ptr(), d_out.data_ptr(), cap, d_fb.data_ptr(), d_off.data_ptr(),
+                                  d_tot.data_ptr(), d_state.data_ptr(), d_md5.data_ptr(), stream=st.cuda_stream)
+    elif md5 == "async":
+        ms = torch.cuda.Stream(dev)
+        enc.encode_plan_device(plan, d_pcm.data_ptr(), d_out.data_ptr(), cap, d_fb.data_ptr(), d_off.data_ptr(),
+                               d_tot.data_ptr(), d_md5.data_ptr(), st.cuda_stream, md5_stream=ms.cuda_stream)
+        ms.synchronize()
+        d_state = None
+    else:
+        enc.encode_plan_device(plan, d_pcm.data_ptr(), d_out.data_ptr(), cap, d_fb.data_ptr(), d_off.data_ptr(),
+                               d_tot.data_ptr(), d_md5.data_ptr() if md5 == "join" else None, st.cuda_stream)
+        d_state = None
+    enc.sync_check(st.cuda_stream)
+    total = int(d_tot[0].item())
+    out = d_out[:total].cpu().numpy().tobytes()
+    fb = d_fb.cpu().numpy()
+    fo = d_off.cpu().numpy()
+    res = []
+    for s in range(len(offs)):
+        f0 = plan.first_frame[s]
+        f1 = plan.first_frame[s + 1] if s + 1 < len(offs) else int(plan.n_frames)
+        a = int(fo[f0]) if f0 < int(plan.n_frames) else total
+        b = int(fo[f1]) if f1 < int(plan.n_frames) else total
+        res.append((out[a:b], [int(x) for x in fb[f0:f1]], d_md5[16 * s:16 * s + 16].cpu().numpy().tobytes()))
+    # offsets are an exclusive scan of the sizes, the total their sum
+    assert int(fb[: int(plan.n_frames)].astype(np.int64).sum()) == total
+    plan.close()
+    return res, d_state
+
+
+def _encoder(ch, bits, rate, max_frames=64, **kw):
+    import flacgpu
+
+    return flacgpu.Encoder(ch, bits, rate, device=0, max_frames=max_frames, **kw)
+
+
+LENGTHS = [0, 1, 3, 4096, 5000, 8192, 4095, 3 * 4096 + 77, 1152, 4097, 6 * 4096, 255, 2 * 4096 + 4095, 64, 12345]
+
+
+@pytest.mark.parametrize("ch,bits,rate,lpc", [(2, 16, 44100, 0), (2, 24, 96000, 0), (1, 16, 48000, 0),
+                                              (2, 32, 192000, 0), (8, 24, 96000, 0), (2, 24, 96000, 8)])
+@pytest.mark.parametrize("aligns", [(0,), (4, 8, 12, 0)])
+def test_plan_streams_match_oracle(ch, bits, rate, lpc, aligns):
+    fb = ch * (bits // 8)
+    offs, size = _layout(LENGTHS, fb, aligns)
+    buf = bytearray(size)
+    pcms = []
+    for s, n in enumerate(LENGTHS):
+        pcm = synth.synth_pcm(n, ch, bits, rate, stream=s) if n else b""
+        buf[offs[s]:offs[s] + len(pcm)] = pcm
+        pcms.append(pcm)
+    with _encoder(ch, bits, rate, lpc_order=lpc) as enc:  # 64 frames per context < the plan's frames
+        res, _ = _run_plan(enc, bytes(buf), offs, LENGTHS)
+    for s, (got, sizes, md5) in enumerate(res):
+        ref, ref_sizes, ref_md5 = oracle_ref.encode_stream(pcms[s], ch, bits, rate, lpc=lpc)
+        assert sizes == ref_sizes, f"stream {s}: frame sizes differ"
+        assert got == ref, f"stream {s}: bytes differ"
+        assert md5 == ref_md5 == hashlib.md5(pcms[s]).digest(), f"stream {s}: MD5"
+
+
+@pytest.mark.parametrize("md5", ["join", "async", "none", "state"])
+def test_plan_md5_schedules(md5):
+    ch, bits, rate = 2, 16, 44100
+    lengths = [4096 * 8] * 40 + [4096 * 3 + 100] * 9 + [1]
+    offs, size = _layout(lengths, 4, (0, 4))
+    buf = bytearray(size)
+    pcms = []
+    for s, n in enumerate(lengths):
+        pcm = synth.synth_pcm(n, ch, bits, rate, stream=100 + s)
+        buf[offs[s]:offs[s] + len(pcm)] = pcm
+        pcms.append(pcm)
+    with _encoder(ch, bits, rate, max_frames=512) as enc:
+        res, _ = _run_plan(enc, bytes(buf), offs, lengths, md5=md5)
+    for s, (got, sizes, dig) in enumerate(res):
+        ref, ref_sizes, ref_md5 = oracle_ref.encode_stream(pcms[s], ch, bits, rate)
+        assert sizes == ref_sizes and got == ref, f"stream {s}"
+        if md5 != "none":
+            assert dig == ref_md5, f"stream {s}: MD5"
+        else:
+            assert dig == bytes(16)
+
+
+@pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (2, 24, 96000), (8, 24, 96000), (2, 32, 192000)])
+def test_streams_spanning_calls_carry_md5_state(ch, bits, rate):
+    """Each stream is cut into segments encoded by successive calls: frame numbers continue,
+    the MD5 state is carried on the device, only the last segment is padded."""
+    torch, dev = _torch()
+    import flacgpu
+
+    fb = ch * (bits // 8)
+    totals = [4096 * 7 + 1234, 4096 * 5, 4096 * 2 + 1, 4096 * 9 + 4095, 4096]
+    seg_frames = [3, 2, 1, 4, 1]  # whole frames per non-final segment, per stream
+    full = [synth.synth_pcm(n, ch, bits, rate, stream=300 + s) for s, n in enumerate(totals)]
+    pos = [0] * len(totals)
+    fnum = [0] * len(totals)
+    outs = [b""] * len(totals)
+    sizes = [[] for _ in totals]
+    state = torch.from_numpy(np.frombuffer(flacgpu.md5_states(len(totals)), dtype=np.uint8).copy()).to(dev)
+    digest = [None] * len(totals)
+    with _encoder(ch, bits, rate, max_frames=32) as enc:
+        while any(pos[s] < totals[s] or digest[s] is None for s in range(len(totals))):
+            # every stream advances by its segment length (streams that are done take an empty final segment)
+            lens, fin = [], []
+            for s in range(len(totals)):
+                left = totals[s] - pos[s]
+                take = min(left, seg_frames[s] * 4096)
+                last = take == left
+                lens.append(take if digest[s] is None else 0)
+                fin.append(last)
+            offs, size = _layout(lens, fb, (4, 0))
+            buf = bytearray(size)
+            for s in range(len(totals)):
+                a = pos[s] * fb
+                buf[offs[s]:offs[s] + lens[s] * fb] = full[s][a:a + lens[s] * fb]
+            res, state = _run_plan(enc, bytes(buf), offs, lens, md5="state", first_frames=fnum, final=fin,
+                                   states=state)
+            for s, (got, sz, dig) in enumerate(res):
+                if digest[s] is not None:
+                    continue
+                outs[s] += got
+                sizes[s] += sz
+                pos[s] += lens[s]
+                fnum[s] += (lens[s] + 4095) // 4096
+                if fin[s]:
+                    digest[s] = dig
+    for s in range(len(totals)):
+        ref, ref_sizes, ref_md5 = oracle_ref.encode_stream(full[s], ch, bits, rate)
+        assert sizes[s] == ref_sizes and outs[s] == ref, f"stream {s}"
+        assert digest[s] == ref_md5 == hashlib.md5(full[s]).digest(), f"stream {s}: carried MD5"
+
+
+def test_non_final_segment_must_be_whole_frames():
+    import flacgpu
+
+    with _encoder(2, 16, 44100) as enc:
+        with pytest.raises(flacgpu.FlacGpuError):
+            enc.plan([0], [4096 + 5], final=[False])
+        with pytest.raises(flacgpu.FlacGpuError):  # offsets are 4-byte aligned
+            enc.plan([2], [4096])
+        with pytest.raises(flacgpu.FlacGpuError):  # u36 frame numbers
+            enc.plan([0], [8192], first_frames=[(1 << 36) - 1])
+
+
+@pytest.mark.parametrize("delta", [1, 127, 2048, (1 << 31) + 5])
+def test_plan_advance_renumbers_frames(delta):
+    ch, bits, rate = 2, 16, 44100
+    lengths = [4096 * 4, 4096 * 2 + 9]
+    offs, size = _layout(lengths, 4, (0,))
+    buf = bytearray(size)
+    pcms = []
+    for s, n in enumerate(lengths):
+        pcm = synth.synth_pcm(n, ch, bits, rate, stream=7 + s)
+        buf[offs[s]:offs[s] + len(pcm)] = pcm
+        pcms.append(pcm)
+    with _encoder(ch, bits, rate) as enc:
+        res, _ = _run_plan(enc, bytes(buf), offs, lengths, first_frames=[10, 0], advance=delta)
+    for s, (got, sizes, _) in enumerate(res):
+        ref, ref_sizes, _ = oracle_ref.encode_stream(pcms[s], ch, bits, rate, first_frame=[10, 0][s] + delta)
+        assert sizes == ref_sizes and got == ref, f"stream {s}"
+
+
+def test_sync_check_reports_output_too_small():
+    import flacgpu
+
+    ch, bits, rate = 2, 16, 44100
+    lengths = [4096 * 16]
+    pcm = synth.synth_pcm(lengths[0], ch, bits, rate)
+    with _encoder(ch, bits, rate) as enc:
+        with pytest.raises(flacgpu.FlacGpuError) as e:
+            _run_plan(enc, pcm + bytes(64), [0], lengths, out_cap=4096)
+        assert e.value.code == -4
+        # the error word is cleared: the next call is clean
+        res, _ = _run_plan(enc, pcm + bytes(64), [0], lengths)
+        ref, _, _ = oracle_ref.encode_stream(pcm, ch, bits, rate)
+        assert res[0][0] == ref

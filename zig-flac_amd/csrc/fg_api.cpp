@@ -9,20 +9,24 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
 #include "../../include/flacgpu.h"
 #include "fg_common.hpp"
+#include "fg_internal.hpp"
 #include "fg_layout.hpp"
+#include "fg_md5_host.hpp"
 
 namespace fg {
 hipError_t launch_stage(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
 hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, uint32_t stride, uint64_t first,
                             uint32_t n_frames, hipStream_t st);
 hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, hipStream_t st);
-hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, uint32_t n,
-                              uint8_t *digests, hipStream_t st);
+hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *fin,
+                              uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st);
+hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipStream_t st);
 hipError_t launch_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks, hipStream_t st);
 }  // namespace fg
 
@@ -30,6 +34,7 @@ using namespace fg;
 
 static_assert(sizeof(SubRec) == sizeof(flacgpu_subframe_record), "record layout");
 static_assert(sizeof(FrameRec) == sizeof(flacgpu_frame_record), "record layout");
+static_assert(sizeof(Md5State) == sizeof(flacgpu_md5_state), "md5 state layout");
 
 namespace {
 
@@ -94,14 +99,19 @@ struct flacgpu_ctx {
     std::vector<hipEvent_t> event_pool;
     uint64_t launches[FLACGPU_K_COUNT] = {};
     double ms[FLACGPU_K_COUNT] = {};
-    // streaming MD5 (one stream)
+    // streaming MD5 (one stream): a host core by default (FLACGPU_MD5_HOST), or one GPU
+    // lane fed by bounded chunks (FLACGPU_MD5_DEVICE, opt-in)
+    int md5_engine = FLACGPU_MD5_HOST;
+    HostMd5 host_md5;
     uint32_t *d_md5_state = nullptr;
     uint32_t *d_md5_blocks = nullptr;
-    uint64_t md5_block_cap = 0;
     uint8_t md5_buf[64] = {};
     uint32_t md5_fill = 0;
     uint64_t md5_len = 0;
 };
+
+// device MD5 engine: whole blocks move through one bounded device buffer
+constexpr uint64_t kMd5ChunkBlocks = (64ull << 20) / 64;
 
 struct flacgpu_plan {
     flacgpu_ctx *ctx = nullptr;
@@ -110,6 +120,8 @@ struct flacgpu_plan {
     uint64_t n_frames = 0, n_full = 0, n_tail = 0;
     FrameJob *d_jobs = nullptr;  // full jobs first, then tail jobs
     uint64_t *d_md5_offs = nullptr, *d_md5_lens = nullptr;
+    uint8_t *d_md5_fin = nullptr;  // per-stream final-segment flags (NULL: all final)
+    uint64_t max_number = 0;       // largest frame number in the table (u36 check on advance)
     std::vector<uint64_t> first_frame;
     uint64_t out_bound = 0;
     uint8_t *d_desc = nullptr;  // per-plan descriptor area when larger than the context's
@@ -282,6 +294,41 @@ int fetch_records(flacgpu_ctx *c, uint64_t n_frames, hipStream_t st) {
 }
 
 }  // namespace
+
+// One chunk of at most max_frames frames (fg_internal.hpp): upload, encode, wait; the
+// frames stay in the context's device output until ctx_download_chunk.
+int fg::ctx_encode_chunk(flacgpu_ctx *c, const uint8_t *src, uint64_t ns, uint64_t first_number, uint64_t *total,
+                         uint32_t *frame_bytes) {
+    const uint32_t bs = c->cfg.block_size;
+    const uint64_t nf = frames_for(ns, bs);
+    if (nf > c->max_frames || !total) return FLACGPU_ERR_INVALID_INPUT;
+    *total = 0;
+    if (nf == 0) return FLACGPU_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->d_pcm, src, ns * c->C * c->B, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)((uint64_t)bs * c->C * c->B), first_number, (uint32_t)nf,
+                            c->stream));
+    // frames with n == 4096 take the lane-owned-partition kernel, the rest the general one
+    const uint64_t n_full = (bs == (uint32_t)kBlock) ? ns / kBlock : 0;
+    int rc = encode_core(c, c->d_pcm, c->d_jobs, n_full, nf - n_full, c->d_desc, c->d_fbytes, c->d_out, c->out_cap,
+                         c->d_offsets, c->d_total, c->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(total, c->d_total, 8, hipMemcpyDeviceToHost, c->stream));
+    if (frame_bytes) HIPCHK(hipMemcpyAsync(frame_bytes, c->d_fbytes, nf * 4, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = fetch_records(c, nf, c->stream))) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return check_device_error(c);
+}
+
+int fg::ctx_download_chunk(flacgpu_ctx *c, uint8_t *out, uint64_t total) {
+    if (!total) return FLACGPU_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(out, c->d_out, total, hipMemcpyDeviceToHost));
+    return FLACGPU_OK;
+}
+
+uint32_t fg::ctx_max_frames(const flacgpu_ctx *c) { return c->max_frames; }
+void fg::ctx_finish(flacgpu_ctx *c) { resolve_timing(c); }
 
 extern "C" {
 
@@ -542,7 +589,12 @@ static int encode_frames_pipelined(flacgpu_ctx *c, const uint8_t *src, uint64_t 
             worker.join();
             if ((rc = wrc)) break;
         }
-        worker = std::thread(download, set, frame0, nf);
+        try {
+            worker = std::thread(download, set, frame0, nf);
+        } catch (const std::system_error &) {
+            download(set, frame0, nf);  // no thread to be had: download in line
+            if ((rc = wrc)) break;
+        }
         frame0 += nf;
     }
     if (worker.joinable()) {
@@ -581,28 +633,17 @@ int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sa
         resolve_timing(c);
         return rc;
     }
+    (void)stride;
     while (frame0 < total_frames) {
         const uint64_t nf = std::min<uint64_t>(c->max_frames, total_frames - frame0);
         const uint64_t s0 = frame0 * bs;
         const uint64_t ns = std::min<uint64_t>(nf * bs, n_samples - s0);
-        const uint64_t nbytes = ns * c->C * c->B;
-        HIPCHK(hipMemcpyAsync(c->d_pcm, src + s0 * c->C * c->B, nbytes, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, first_frame_number + frame0, (uint32_t)nf,
-                                c->stream));
-        // frames with n == 4096 take the lane-owned-partition kernel, the rest the general one
-        uint64_t n_full = (bs == (uint32_t)kBlock) ? ns / kBlock : 0;
-        int rc = encode_core(c, c->d_pcm, c->d_jobs, n_full, nf - n_full, c->d_desc, c->d_fbytes, c->d_out,
-                             c->out_cap, c->d_offsets, c->d_total, c->stream);
-        if (rc) return rc;
         uint64_t total = 0;
-        HIPCHK(hipMemcpyAsync(&total, c->d_total, 8, hipMemcpyDeviceToHost, c->stream));
-        if (frame_bytes)
-            HIPCHK(hipMemcpyAsync(frame_bytes + frame0, c->d_fbytes, nf * 4, hipMemcpyDeviceToHost, c->stream));
-        if ((rc = fetch_records(c, nf, c->stream))) return rc;
-        HIPCHK(hipStreamSynchronize(c->stream));
-        if ((rc = check_device_error(c))) return rc;
+        int rc = fg::ctx_encode_chunk(c, src + s0 * c->C * c->B, ns, first_frame_number + frame0, &total,
+                                      frame_bytes ? frame_bytes + frame0 : nullptr);
+        if (rc) return rc;
         if (written + total > out_cap) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
-        HIPCHK(hipMemcpy(out + written, c->d_out, total, hipMemcpyDeviceToHost));
+        if ((rc = fg::ctx_download_chunk(c, out + written, total))) return rc;
         written += total;
         frame0 += nf;
     }
@@ -633,36 +674,48 @@ int flacgpu_encode_frame_planar(flacgpu_ctx *c, const int32_t *const planes[8], 
 }
 
 // ---- streaming MD5 --------------------------------------------------------
+int flacgpu_md5_set_engine(flacgpu_ctx *c, int engine) {
+    if (!c || (engine != FLACGPU_MD5_HOST && engine != FLACGPU_MD5_DEVICE)) return FLACGPU_ERR_INVALID_INPUT;
+    c->md5_engine = engine;
+    return flacgpu_md5_init(c);
+}
+
+int flacgpu_md5_get_engine(const flacgpu_ctx *c) { return c ? c->md5_engine : FLACGPU_ERR_INVALID_INPUT; }
+
 int flacgpu_md5_init(flacgpu_ctx *c) {
     if (!c) return FLACGPU_ERR_INVALID_INPUT;
+    c->host_md5.reset();
+    c->md5_fill = 0;
+    c->md5_len = 0;
+    if (c->md5_engine != FLACGPU_MD5_DEVICE) return FLACGPU_OK;
     const uint32_t iv[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpy(c->d_md5_state, iv, 16, hipMemcpyHostToDevice));
-    c->md5_fill = 0;
-    c->md5_len = 0;
     return FLACGPU_OK;
 }
 
+// device engine: whole blocks through one bounded buffer (kMd5ChunkBlocks per launch)
 static int md5_push_blocks(flacgpu_ctx *c, const uint8_t *p, uint64_t nblocks) {
     if (!nblocks) return FLACGPU_OK;
-    if (nblocks > c->md5_block_cap) {
-        hipFree(c->d_md5_blocks);
-        c->d_md5_blocks = nullptr;
-        c->md5_block_cap = 0;
-        HIPCHK(hipMalloc(&c->d_md5_blocks, nblocks * 64));
-        c->md5_block_cap = nblocks;
+    if (!c->d_md5_blocks) HIPCHK(hipMalloc(&c->d_md5_blocks, kMd5ChunkBlocks * 64));
+    for (uint64_t b = 0; b < nblocks; b += kMd5ChunkBlocks) {
+        const uint64_t nb = std::min<uint64_t>(kMd5ChunkBlocks, nblocks - b);
+        HIPCHK(hipMemcpyAsync(c->d_md5_blocks, p + b * 64, nb * 64, hipMemcpyHostToDevice, c->stream));
+        {
+            Timed t(c, FLACGPU_K_MD5, c->stream);
+            HIPCHK(launch_md5_blocks(c->d_md5_state, c->d_md5_blocks, nb, c->stream));
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
     }
-    HIPCHK(hipMemcpyAsync(c->d_md5_blocks, p, nblocks * 64, hipMemcpyHostToDevice, c->stream));
-    {
-        Timed t(c, FLACGPU_K_MD5, c->stream);
-        HIPCHK(launch_md5_blocks(c->d_md5_state, c->d_md5_blocks, nblocks, c->stream));
-    }
-    HIPCHK(hipStreamSynchronize(c->stream));
     return FLACGPU_OK;
 }
 
 int flacgpu_md5_update(flacgpu_ctx *c, const void *data, size_t len) {
     if (!c || (!data && len)) return FLACGPU_ERR_INVALID_INPUT;
+    if (c->md5_engine != FLACGPU_MD5_DEVICE) {
+        c->host_md5.update(data, len);
+        return FLACGPU_OK;
+    }
     HIPCHK(hipSetDevice(c->device));
     const uint8_t *p = (const uint8_t *)data;
     c->md5_len += len;
@@ -690,6 +743,10 @@ int flacgpu_md5_update(flacgpu_ctx *c, const void *data, size_t len) {
 
 int flacgpu_md5_final(flacgpu_ctx *c, uint8_t digest[16]) {
     if (!c || !digest) return FLACGPU_ERR_INVALID_INPUT;
+    if (c->md5_engine != FLACGPU_MD5_DEVICE) {
+        c->host_md5.final(digest);
+        return FLACGPU_OK;
+    }
     HIPCHK(hipSetDevice(c->device));
     uint8_t tail[128] = {};
     std::memcpy(tail, c->md5_buf, c->md5_fill);
@@ -707,9 +764,22 @@ int flacgpu_md5_final(flacgpu_ctx *c, uint8_t digest[16]) {
     return flacgpu_md5_init(c);
 }
 
+void flacgpu_md5_state_init(flacgpu_md5_state *s, size_t n) {
+    for (size_t i = 0; s && i < n; i++) {
+        s[i].h[0] = 0x67452301u;
+        s[i].h[1] = 0xefcdab89u;
+        s[i].h[2] = 0x98badcfeu;
+        s[i].h[3] = 0x10325476u;
+        s[i].bytes = 0;
+        s[i].finished = 0;
+        s[i].reserved = 0;
+    }
+}
+
 // ---- plans (device-resident batches of independent streams) --------------
-int flacgpu_plan_create(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs, const uint64_t *samples,
-                        uint32_t bytes_per_sample, flacgpu_plan **out) {
+int flacgpu_plan_create_segments(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs, const uint64_t *samples,
+                                 uint32_t bytes_per_sample, const uint64_t *first_frame_numbers,
+                                 const uint8_t *final_segment, flacgpu_plan **out) {
     if (!c || !out || (n_streams && (!offs || !samples)) || bytes_per_sample != c->B) return FLACGPU_ERR_INVALID_INPUT;
     *out = nullptr;
     HIPCHK(hipSetDevice(c->device));
@@ -717,39 +787,56 @@ int flacgpu_plan_create(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs
     const uint64_t fbytes_in = (uint64_t)c->C * c->B;
     std::vector<FrameJob> full, tail;
     std::vector<uint64_t> lens(n_streams);
+    uint64_t max_number = 0;
+    // validate everything before any allocation
+    for (uint32_t s = 0; s < n_streams; s++) {
+        // stream starts: 4-byte aligned (the kernels' dword / 16-byte vector loads)
+        if (offs[s] & 3u) return FLACGPU_ERR_INVALID_INPUT;
+        const uint64_t nf = frames_for(samples[s], bs);
+        const uint64_t f0 = first_frame_numbers ? first_frame_numbers[s] : 0;
+        if (nf && (f0 >= (1ull << 36) || nf - 1 > (1ull << 36) - 1 - f0)) return FLACGPU_ERR_INVALID_INPUT;  // u36
+        if (nf) max_number = std::max(max_number, f0 + nf - 1);
+        // a segment that the stream continues after: whole frames and whole MD5 blocks
+        if (final_segment && !final_segment[s] && (samples[s] % bs || (samples[s] * fbytes_in) % 64))
+            return FLACGPU_ERR_INVALID_INPUT;
+    }
     auto *p = new (std::nothrow) flacgpu_plan();
     if (!p) return FLACGPU_ERR_OUT_OF_MEMORY;
     p->ctx = c;
     p->n_streams = n_streams;
     p->B = bytes_per_sample;
-    p->first_frame.resize(n_streams);
+    p->max_number = max_number;
     uint64_t slot = 0;
-    for (uint32_t s = 0; s < n_streams; s++) {
-        if (offs[s] & 3u) {
-            delete p;
-            return FLACGPU_ERR_INVALID_INPUT;
+    try {
+        p->first_frame.resize(n_streams);
+        for (uint32_t s = 0; s < n_streams; s++) {
+            p->first_frame[s] = slot;
+            lens[s] = samples[s] * fbytes_in;
+            const uint64_t nf = frames_for(samples[s], bs);
+            const uint64_t f0 = first_frame_numbers ? first_frame_numbers[s] : 0;
+            for (uint64_t f = 0; f < nf; f++, slot++) {
+                FrameJob j;
+                j.pcm_off = offs[s] + f * bs * fbytes_in;
+                j.number = f0 + f;
+                j.n = (uint32_t)std::min<uint64_t>(bs, samples[s] - f * bs);
+                j.slot = (uint32_t)slot;
+                (j.n == (uint32_t)kBlock ? full : tail).push_back(j);
+            }
         }
-        p->first_frame[s] = slot;
-        lens[s] = samples[s] * fbytes_in;
-        const uint64_t nf = frames_for(samples[s], bs);
-        for (uint64_t f = 0; f < nf; f++, slot++) {
-            FrameJob j;
-            j.pcm_off = offs[s] + f * bs * fbytes_in;
-            j.number = f;
-            j.n = (uint32_t)std::min<uint64_t>(bs, samples[s] - f * bs);
-            j.slot = (uint32_t)slot;
-            (j.n == (uint32_t)kBlock ? full : tail).push_back(j);
-        }
+        full.insert(full.end(), tail.begin(), tail.end());
+    } catch (...) {
+        delete p;
+        return FLACGPU_ERR_OUT_OF_MEMORY;
     }
     p->n_frames = slot;
-    p->n_full = full.size();
+    p->n_full = full.size() - tail.size();
     p->n_tail = tail.size();
     p->out_bound = slot * (uint64_t)c->image_bytes;
-    full.insert(full.end(), tail.begin(), tail.end());
     auto fail = [&](int code) {
         flacgpu_plan_destroy(p);
         return code;
     };
+    if (slot > 0xFFFFFFFFull) return fail(FLACGPU_ERR_INVALID_INPUT);
     if (slot) {
         if (hipMalloc(&p->d_jobs, slot * sizeof(FrameJob))) return fail(FLACGPU_ERR_OUT_OF_MEMORY);
         if (hipMemcpy(p->d_jobs, full.data(), slot * sizeof(FrameJob), hipMemcpyHostToDevice))
@@ -761,6 +848,10 @@ int flacgpu_plan_create(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs
         if (hipMemcpy(p->d_md5_offs, offs, n_streams * 8, hipMemcpyHostToDevice) ||
             hipMemcpy(p->d_md5_lens, lens.data(), n_streams * 8, hipMemcpyHostToDevice))
             return fail(FLACGPU_ERR_DEVICE);
+        if (final_segment) {
+            if (hipMalloc(&p->d_md5_fin, n_streams)) return fail(FLACGPU_ERR_OUT_OF_MEMORY);
+            if (hipMemcpy(p->d_md5_fin, final_segment, n_streams, hipMemcpyHostToDevice)) return fail(FLACGPU_ERR_DEVICE);
+        }
     }
     if (slot > c->max_frames && hipMalloc(&p->d_desc, slot * (uint64_t)c->desc_stride))
         return fail(FLACGPU_ERR_OUT_OF_MEMORY);
@@ -768,11 +859,17 @@ int flacgpu_plan_create(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs
     return FLACGPU_OK;
 }
 
+int flacgpu_plan_create(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs, const uint64_t *samples,
+                        uint32_t bytes_per_sample, flacgpu_plan **out) {
+    return flacgpu_plan_create_segments(c, n_streams, offs, samples, bytes_per_sample, nullptr, nullptr, out);
+}
+
 void flacgpu_plan_destroy(flacgpu_plan *p) {
     if (!p) return;
     hipFree(p->d_jobs);
     hipFree(p->d_md5_offs);
     hipFree(p->d_md5_lens);
+    hipFree(p->d_md5_fin);
     hipFree(p->d_desc);
     delete p;
 }
@@ -783,11 +880,26 @@ uint64_t flacgpu_plan_stream_first_frame(const flacgpu_plan *p, uint32_t s) {
     return (p && s < p->n_streams) ? p->first_frame[s] : 0;
 }
 
-int flacgpu_encode_plan_device_md5_async(flacgpu_ctx *c, const flacgpu_plan *p, const void *d_pcm, uint8_t *d_out,
-                                         uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets,
-                                         uint64_t *d_total, uint8_t *d_md5, void *hip_stream, void *md5_stream) {
+int flacgpu_plan_advance(flacgpu_plan *p, uint64_t frames, void *hip_stream) {
+    if (!p) return FLACGPU_ERR_INVALID_INPUT;
+    if (!frames || !p->n_frames) return FLACGPU_OK;
+    if (frames > (1ull << 36) - 1 - p->max_number) return FLACGPU_ERR_INVALID_INPUT;  // u36 frame numbers
+    flacgpu_ctx *c = p->ctx;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    HIPCHK(launch_advance_jobs(p->d_jobs, p->n_frames, frames, st));
+    p->max_number += frames;
+    return FLACGPU_OK;
+}
+
+int flacgpu_encode_plan_device_ex(flacgpu_ctx *c, const flacgpu_plan *p, const void *d_pcm, uint8_t *d_out,
+                                  uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets,
+                                  uint64_t *d_total, flacgpu_md5_state *d_md5_state, uint8_t *d_md5, void *hip_stream,
+                                  void *md5_stream) {
     if (!c || !p || p->ctx != c || !d_pcm || !d_out || !d_frame_bytes || !d_frame_offsets || !d_total)
         return FLACGPU_ERR_INVALID_INPUT;
+    // a stream that continues past this segment has no digest yet: its state must be carried
+    if (p->d_md5_fin && d_md5 && !d_md5_state) return FLACGPU_ERR_INVALID_INPUT;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     if (c->records_on && p->n_frames > c->max_frames) return FLACGPU_ERR_INVALID_INPUT;
@@ -796,7 +908,8 @@ int flacgpu_encode_plan_device_md5_async(flacgpu_ctx *c, const flacgpu_plan *p, 
     // st unless the caller owns the MD5 stream)
     const bool join = md5_stream == nullptr;
     hipStream_t ms = join ? c->aux : (hipStream_t)md5_stream;
-    if (d_md5 && p->n_streams) {
+    const bool md5 = (d_md5 || d_md5_state) && p->n_streams;
+    if (md5) {
         hipEvent_t fork = join ? c->fork : get_event(c);
         if (!fork) return FLACGPU_ERR_DEVICE;
         HIPCHK(hipEventRecord(fork, st));
@@ -804,22 +917,37 @@ int flacgpu_encode_plan_device_md5_async(flacgpu_ctx *c, const flacgpu_plan *p, 
         if (!join) c->event_pool.push_back(fork);  // recycled: the wait is already enqueued
         {
             Timed t(c, FLACGPU_K_MD5, ms);
-            HIPCHK(launch_md5_streams((const uint8_t *)d_pcm, p->d_md5_offs, p->d_md5_lens, p->n_streams, d_md5, ms));
+            HIPCHK(launch_md5_streams((const uint8_t *)d_pcm, p->d_md5_offs, p->d_md5_lens, p->d_md5_fin, p->n_streams,
+                                      (Md5State *)d_md5_state, d_md5, ms));
         }
         if (join) HIPCHK(hipEventRecord(c->join, ms));
     }
     int rc = encode_core(c, (const uint8_t *)d_pcm, p->d_jobs, p->n_full, p->n_tail, desc, d_frame_bytes, d_out,
                          out_cap, d_frame_offsets, d_total, st);
     if (rc) return rc;
-    if (join && d_md5 && p->n_streams) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
+    if (join && md5) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
     return FLACGPU_OK;
+}
+
+int flacgpu_encode_plan_device_md5_async(flacgpu_ctx *c, const flacgpu_plan *p, const void *d_pcm, uint8_t *d_out,
+                                         uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets,
+                                         uint64_t *d_total, uint8_t *d_md5, void *hip_stream, void *md5_stream) {
+    return flacgpu_encode_plan_device_ex(c, p, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total, nullptr,
+                                         d_md5, hip_stream, md5_stream);
 }
 
 int flacgpu_encode_plan_device(flacgpu_ctx *c, const flacgpu_plan *p, const void *d_pcm, uint8_t *d_out,
                                uint64_t out_cap, uint32_t *d_frame_bytes, uint64_t *d_frame_offsets, uint64_t *d_total,
                                uint8_t *d_md5, void *hip_stream) {
-    return flacgpu_encode_plan_device_md5_async(c, p, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total,
-                                                d_md5, hip_stream, nullptr);
+    return flacgpu_encode_plan_device_ex(c, p, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total, nullptr,
+                                         d_md5, hip_stream, nullptr);
+}
+
+int flacgpu_sync_check(flacgpu_ctx *c, void *hip_stream) {
+    if (!c) return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(hip_stream ? (hipStream_t)hip_stream : c->stream));
+    return check_device_error(c);
 }
 
 // ---- instrumentation ---------------------------------------------------------

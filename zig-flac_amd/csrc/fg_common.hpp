@@ -25,6 +25,15 @@ struct FrameJob {
     uint32_t slot;      // output slot / frame index within the call
 };
 
+// Per-stream MD5 chaining state carried across calls (mirrors flacgpu_md5_state).
+struct Md5State {
+    uint32_t h[4];
+    uint64_t bytes;     // message bytes absorbed so far
+    uint32_t flags;     // 1 once the stream's final segment has been padded
+    uint32_t pad;
+};
+static_assert(sizeof(Md5State) == 32, "Md5State layout");
+
 // Per-candidate decision record (SubframeType.Encoding + estimate,
 // encoder.zig:678-702).  Mirrors flacgpu_subframe_record.
 struct SubRec {

@@ -8,9 +8,12 @@
 // here.
 #include <algorithm>
 #include <cstring>
+#include <system_error>
+#include <thread>
 #include <vector>
 
 #include "../../include/flacgpu.h"
+#include "fg_md5_host.hpp"
 
 namespace {
 
@@ -143,7 +146,10 @@ size_t flacgpu_vorbis_comment_bytes(int last_metadata, uint8_t out[31]) {
 
 // wav2flac.main + encode (wav2flac.zig:10-97) for PCM already in memory: skipHeader,
 // writeVorbisComment(true), every frame through the GPU (sizes replayed into
-// updateFrameSize in frame order), MD5 on the GPU, then the header written last.
+// updateFrameSize in frame order), the MD5 of the PCM bytes, then the header written
+// last.  With the host MD5 engine (the default) the hash runs on its own thread while
+// the GPU encodes (the reference interleaves the two per block on one thread,
+// wav_reader.zig:66 beside encoder.zig:234); the device engine hashes after the encode.
 int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
                         uint8_t *out, size_t out_cap, size_t *out_len) {
     if (!ctx || !out || !out_len || (!pcm && n_samples)) return FLACGPU_ERR_INVALID_INPUT;
@@ -152,19 +158,41 @@ int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sa
     int rc = flacgpu_get_config(ctx, &cfg);
     if (rc) return rc;
     if (out_cap < 73) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
+    if (bytes_per_sample != cfg.bits_per_sample / 8u) return FLACGPU_ERR_INVALID_INPUT;
     const uint64_t block = cfg.block_size;
     const uint64_t n_frames = (n_samples + block - 1) / block;
-    std::vector<uint32_t> sizes(n_frames ? n_frames : 1);
+    const size_t pcm_bytes = (size_t)(n_samples * cfg.channels * bytes_per_sample);
+    std::vector<uint32_t> sizes;
+    try {
+        sizes.resize(n_frames ? n_frames : 1);
+    } catch (...) {
+        return FLACGPU_ERR_OUT_OF_MEMORY;
+    }
+    flacgpu_streaminfo si;
+    flacgpu_streaminfo_init(&si, cfg.sample_rate, cfg.channels, cfg.bits_per_sample, n_samples, cfg.block_size);
+    fg::HostMd5 md5;
+    std::thread hasher;
+    const bool host_md5 = flacgpu_md5_get_engine(ctx) == FLACGPU_MD5_HOST;
+    if (host_md5) {
+        try {
+            hasher = std::thread([&]() { md5.update(pcm, pcm_bytes); });
+        } catch (const std::system_error &) {
+            md5.update(pcm, pcm_bytes);  // no thread to be had: hash here, before the encode
+        }
+    }
     size_t frames_len = 0;
     rc = flacgpu_encode_frames(ctx, pcm, bytes_per_sample, n_samples, 0, out + 73, out_cap - 73, &frames_len,
                                sizes.data());
+    if (hasher.joinable()) hasher.join();
     if (rc) return rc;
-    flacgpu_streaminfo si;
-    flacgpu_streaminfo_init(&si, cfg.sample_rate, cfg.channels, cfg.bits_per_sample, n_samples, 4096);
     for (uint64_t f = 0; f < n_frames; f++) flacgpu_streaminfo_update_frame_size(&si, sizes[f]);
-    if ((rc = flacgpu_md5_init(ctx))) return rc;
-    if ((rc = flacgpu_md5_update(ctx, pcm, (size_t)(n_samples * cfg.channels * bytes_per_sample)))) return rc;
-    if ((rc = flacgpu_md5_final(ctx, si.md5))) return rc;
+    if (host_md5) {
+        md5.final(si.md5);
+    } else {
+        if ((rc = flacgpu_md5_init(ctx))) return rc;
+        if ((rc = flacgpu_md5_update(ctx, pcm, pcm_bytes))) return rc;
+        if ((rc = flacgpu_md5_final(ctx, si.md5))) return rc;
+    }
     flacgpu_header_bytes(&si, 0, out);
     flacgpu_vorbis_comment_bytes(1, out + 42);
     *out_len = 73 + frames_len;

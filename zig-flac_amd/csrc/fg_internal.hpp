@@ -1,0 +1,19 @@
+// fg_internal.hpp -- library-internal entry points shared by the translation
+// units behind the C ABI (not exported in include/flacgpu.h).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/flacgpu.h"
+
+namespace fg {
+// Upload ns interleaved samples (at most max_frames frames) from host memory, encode
+// them with frame numbers from first_number, wait; *total = bytes of the encoded
+// frames, now in the context's device output; frame_bytes (if non-NULL) receives the
+// per-frame sizes.  Device-side errors are reported here.
+int ctx_encode_chunk(flacgpu_ctx *c, const uint8_t *src, uint64_t ns, uint64_t first_number, uint64_t *total,
+                     uint32_t *frame_bytes);
+// Copy the last chunk's `total` encoded bytes to host memory at out.
+int ctx_download_chunk(flacgpu_ctx *c, uint8_t *out, uint64_t total);
+uint32_t ctx_max_frames(const flacgpu_ctx *c);
+void ctx_finish(flacgpu_ctx *c);  // fold pending timing events
+}  // namespace fg

@@ -1,0 +1,23 @@
+// fg_md5_host.hpp -- MD5 (RFC 1321) on a host core: the hash the reference's
+// Md5 wrapper computes (std.crypto.hash.Md5 / OpenSSL, src/lib/md5.zig:3-31)
+// over the raw WAV data bytes (wav_reader.zig:66).  One stream is a strictly
+// sequential chain; a host core runs it ~10x faster than one GPU lane, so the
+// host-buffer paths hash here, on a thread beside the GPU encode.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace fg {
+
+struct HostMd5 {
+    uint32_t h[4];
+    uint64_t bytes;
+    uint8_t buf[64];
+    uint32_t fill;
+    HostMd5() { reset(); }
+    void reset();
+    void update(const void *data, size_t len);
+    void final(uint8_t digest[16]);  // pads, writes the digest, resets
+};
+
+}  // namespace fg

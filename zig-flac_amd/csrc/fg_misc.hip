@@ -56,6 +56,12 @@ __global__ void k_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, 
     jobs[f] = j;
 }
 
+// the same streams' next window (flacgpu_plan_advance): frame numbers move on by delta
+__global__ void k_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) jobs[i].number += delta;
+}
+
 // ------------------------------------------------------------------------
 // exclusive scan of frame sizes -> byte offsets (single workgroup, 1024 thr).
 // Thread t owns a contiguous run of `per` sizes (a multiple of 4), read as
@@ -179,9 +185,39 @@ __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
 }
 
-// Full digest of n_streams independent byte ranges (offsets 4-byte aligned).
+// MD5 of n_streams independent byte ranges (segments), one lane per stream.
+// A segment may continue a stream begun by an earlier call: `states` (if
+// non-NULL) holds each stream's chaining value and byte count in and out
+// (Md5.update over successive blocks, wav_reader.zig:66).  A non-final segment
+// is a whole number of 64-byte blocks (checked on the host); a final one is
+// padded and its digest written to digests[16 s] (Md5.final,
+// encoder.zig:168-170).  `final_flags` NULL = every segment final.
+// Messages are read as 16-byte vectors (segment starts are 4-byte aligned;
+// the unaligned-access mode of the HSA runtime serves them) and prefetched
+// kMd5Ahead blocks ahead: 4 vector loads per block instead of 16 dword loads
+// keep the texture-address path, which the encode kernels' LDS-DMA staging
+// shares on the same CU, 4x less busy.
+typedef uint32_t md5_v4 __attribute__((ext_vector_type(4), aligned(4)));
+#ifndef FG_MD5_AHEAD
+#define FG_MD5_AHEAD 2
+#endif
+constexpr int kMd5Ahead = FG_MD5_AHEAD;
+
+__device__ __forceinline__ void md5_load_block(const uint8_t *p, uint32_t (&m)[16]) {
+    const md5_v4 *q = (const md5_v4 *)p;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const md5_v4 v = q[i];
+        m[4 * i + 0] = v.x;
+        m[4 * i + 1] = v.y;
+        m[4 * i + 2] = v.z;
+        m[4 * i + 3] = v.w;
+    }
+}
+
 __global__ void __launch_bounds__(64) k_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens,
-                                                    uint32_t n_streams, uint8_t *digests) {
+                                                    const uint8_t *final_flags, uint32_t n_streams, Md5State *states,
+                                                    uint8_t *digests) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_streams) return;
     // The chain is latency-bound (one dependent VALU op every issue slot) and these few
@@ -192,47 +228,72 @@ __global__ void __launch_bounds__(64) k_md5_streams(const uint8_t *base, const u
     __builtin_amdgcn_s_setprio(FG_MD5_PRIO);
     const uint8_t *p = base + offs[s];
     const uint64_t len = lens[s];
+    const bool fin = final_flags ? final_flags[s] != 0 : true;
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    uint64_t done = 0;  // bytes absorbed by earlier segments
+    if (states) {
+        const Md5State in = states[s];
+        st[0] = in.h[0];
+        st[1] = in.h[1];
+        st[2] = in.h[2];
+        st[3] = in.h[3];
+        done = in.bytes;
+    }
     const uint64_t full = len >> 6;
-    const uint32_t *p32 = (const uint32_t *)p;
-    uint32_t m[16];
-    if (full) {
+    // ring of kMd5Ahead + 1 message blocks: block b is consumed while b + 1 .. b + kMd5Ahead load
+    uint32_t m[kMd5Ahead + 1][16];
 #pragma unroll
-        for (int i = 0; i < 16; i++) m[i] = p32[i];
-    }
-    for (uint64_t b = 0; b < full; b++) {
-        // prefetch the next block while this one is compressed
-        uint32_t nx[16];
-        const uint64_t nb_ = (b + 1 < full) ? b + 1 : b;
+    for (int k = 0; k < kMd5Ahead + 1; k++)
+        if ((uint64_t)k < full) md5_load_block(p + 64u * k, m[k]);
+    uint64_t b = 0;
+    for (; b + kMd5Ahead + 1 <= full; b += kMd5Ahead + 1) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) nx[i] = p32[nb_ * 16 + i];
-        md5_compress(st, m);
-#pragma unroll
-        for (int i = 0; i < 16; i++) m[i] = nx[i];
-    }
-    // tail + padding (one or two blocks), assembled straight into message words
-    const uint32_t rem = (uint32_t)(len & 63);
-    const uint8_t *tp = p + full * 64;
-    const uint32_t nb = rem < 56 ? 1u : 2u;
-    const uint64_t bits = len * 8;
-    for (uint32_t b = 0; b < nb; b++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t idx = b * 64u + 4u * i + q;
-                uint32_t by = idx < rem ? tp[idx] : (idx == rem ? 0x80u : 0u);
-                if (b == nb - 1 && 4 * i + q >= 56) by = (uint32_t)(bits >> (8 * (4 * i + q - 56))) & 255u;
-                v |= by << (8 * q);
-            }
-            m[i] = v;
+        for (int k = 0; k < kMd5Ahead + 1; k++) {
+            md5_compress(st, m[k]);
+            const uint64_t nb = b + k + kMd5Ahead + 1;
+            if (nb < full) md5_load_block(p + 64u * nb, m[k]);
         }
-        md5_compress(st, m);
     }
-    for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++) digests[16 * s + 4 * i + j] = (uint8_t)(st[i] >> (8 * j));
+#pragma unroll
+    for (int k = 0; k < kMd5Ahead; k++)
+        if (b + k < full) md5_compress(st, m[k]);
+    if (fin) {
+        // tail + padding (one or two blocks), assembled straight into message words
+        const uint32_t rem = (uint32_t)(len & 63);
+        const uint8_t *tp = p + full * 64;
+        const uint32_t nb = rem < 56 ? 1u : 2u;
+        const uint64_t bits = (done + len) * 8;
+        for (uint32_t bb = 0; bb < nb; bb++) {
+            uint32_t mt[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t idx = bb * 64u + 4u * i + q;
+                    uint32_t by = idx < rem ? tp[idx] : (idx == rem ? 0x80u : 0u);
+                    if (bb == nb - 1 && 4 * i + q >= 56) by = (uint32_t)(bits >> (8 * (4 * i + q - 56))) & 255u;
+                    v |= by << (8 * q);
+                }
+                mt[i] = v;
+            }
+            md5_compress(st, mt);
+        }
+        if (digests)
+            for (int i = 0; i < 4; i++)
+                for (int j = 0; j < 4; j++) digests[16 * s + 4 * i + j] = (uint8_t)(st[i] >> (8 * j));
+    }
+    if (states) {
+        Md5State o;
+        o.h[0] = st[0];
+        o.h[1] = st[1];
+        o.h[2] = st[2];
+        o.h[3] = st[3];
+        o.bytes = done + len;
+        o.flags = fin ? 1u : 0u;
+        o.pad = 0;
+        states[s] = o;
+    }
 }
 
 // Streaming update of one MD5 state in device memory by whole 64-byte blocks.
@@ -259,15 +320,22 @@ hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, 
     return hipGetLastError();
 }
 
+hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_advance_jobs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, jobs, n, delta);
+    return hipGetLastError();
+}
+
 hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, hipStream_t st) {
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, sizes, offsets, total, n);
     return hipGetLastError();
 }
 
-hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, uint32_t n,
-                              uint8_t *digests, hipStream_t st) {
+hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *fin,
+                              uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_md5_streams, dim3((n + 63) / 64), dim3(64), 0, st, base, offs, lens, n, digests);
+    hipLaunchKernelGGL(k_md5_streams, dim3((n + 63) / 64), dim3(64), 0, st, base, offs, lens, fin, n, states,
+                       digests);
     return hipGetLastError();
 }
 

@@ -2,19 +2,60 @@
 // contexts (one per GPU), encoded concurrently and concatenated in frame order.
 // Frame f depends only on its samples and its number (encoder.zig:234-284), so
 // contiguous frame ranges encode independently; the only exchange is the
-// concatenation of the variable-length bitstreams.
+// concatenation of the variable-length bitstreams (SURVEY.md §8(e),
+// wav2flac.zig:66-97 with the frame-order replay of metadata.zig:35-40).
+//
+// The input is cut into rounds of n_ctx x max_frames frames; in a round, context
+// i encodes the i-th contiguous slice.  One host thread per context; after a
+// round's encodes every thread knows all the round's byte counts (a barrier), so
+// each copies its frames from its GPU straight into the caller's buffer at the
+// scanned offset -- no host staging, no second copy.  A thread's download of round
+// r overlaps the other contexts' encodes of round r + 1.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <memory>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
-#include "../../include/flacgpu.h"
+#include "fg_internal.hpp"
 
 struct flacgpu_multi {
     std::vector<flacgpu_ctx *> ctx;
     flacgpu_config cfg{};
 };
+
+namespace {
+
+// Reusable barrier for the worker threads of one call.
+class Barrier {
+  public:
+    explicit Barrier(size_t n) : n_(n) {}
+    void wait() {
+        std::unique_lock<std::mutex> lk(m_);
+        const size_t gen = gen_;
+        if (++count_ == n_) {
+            count_ = 0;
+            gen_++;
+            cv_.notify_all();
+            return;
+        }
+        cv_.wait(lk, [&] { return gen_ != gen; });
+    }
+
+  private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    size_t n_, count_ = 0, gen_ = 0;
+};
+
+}  // namespace
+
+extern "C" {
 
 int flacgpu_open_multi(int n_devices, const int *devices, const flacgpu_config *cfg, uint32_t max_frames_per_call,
                        flacgpu_multi **out) {
@@ -48,49 +89,96 @@ int flacgpu_multi_encode_frames(flacgpu_multi *m, const void *pcm, uint32_t byte
                                 uint32_t *frame_bytes) {
     if (!m || (!pcm && n_samples) || !out_len) return FLACGPU_ERR_INVALID_INPUT;
     *out_len = 0;
-    const uint32_t bs = m->cfg.block_size ? m->cfg.block_size : 4096u;
+    if (bytes_per_sample != m->cfg.bits_per_sample / 8u) return FLACGPU_ERR_INVALID_INPUT;
+    const uint64_t bs = m->cfg.block_size;
     const uint64_t frames = (n_samples + bs - 1) / bs;
+    if (frames && (first_frame_number >= (1ull << 36) || frames - 1 > (1ull << 36) - 1 - first_frame_number))
+        return FLACGPU_ERR_INVALID_INPUT;  // u36 frame numbers
     const uint64_t n = m->ctx.size();
-    const uint64_t per = (frames + n - 1) / (n ? n : 1);
     const uint64_t isz = (uint64_t)m->cfg.channels * bytes_per_sample;  // bytes per interchannel sample
-    const size_t fb = flacgpu_frame_bound_bytes(&m->cfg);
-    struct Part {
-        uint64_t f0 = 0, nf = 0;
-        std::vector<uint8_t> buf;
-        size_t len = 0;
-        int rc = FLACGPU_OK;
+    // frames per context and round: even slices of a round, capped by the context capacity
+    const uint64_t cap = fg::ctx_max_frames(m->ctx[0]);
+    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(cap, (frames + n - 1) / n));
+    const uint64_t rounds = frames ? (frames + per * n - 1) / (per * n) : 0;
+    std::vector<uint64_t> totals;
+    try {
+        totals.assign(rounds * n, 0);
+    } catch (...) {
+        return FLACGPU_ERR_OUT_OF_MEMORY;
+    }
+    // per-context result: set by its own thread, read by all after a barrier
+    std::unique_ptr<std::atomic<int>[]> rcs(new (std::nothrow) std::atomic<int>[n]);
+    if (!rcs) return FLACGPU_ERR_OUT_OF_MEMORY;
+    for (uint64_t i = 0; i < n; i++) rcs[i] = FLACGPU_OK;
+    Barrier bar(n);
+    auto slice = [&](uint64_t r, uint64_t i, uint64_t *f0, uint64_t *nf) {
+        const uint64_t a = std::min(frames, (r * n + i) * per);
+        *f0 = a;
+        *nf = std::min(frames, a + per) - a;
     };
-    std::vector<Part> parts(n);
-    for (uint64_t i = 0; i < n; i++) {  // all staging first: no thread is running on an early return
-        Part &p = parts[i];
-        p.f0 = std::min(frames, i * per);
-        p.nf = std::min(frames, p.f0 + per) - p.f0;
-        if (p.nf == 0) continue;
-        try {
-            p.buf.resize(p.nf * fb + 64);
-        } catch (...) {
-            return FLACGPU_ERR_OUT_OF_MEMORY;
+    auto work = [&](uint64_t i) {
+        flacgpu_ctx *c = m->ctx[i];
+        for (uint64_t r = 0; r < rounds; r++) {
+            uint64_t f0, nf;
+            slice(r, i, &f0, &nf);
+            int rc = FLACGPU_OK;
+            if (nf && !rcs[i]) {
+                const uint64_t s0 = f0 * bs, ns = std::min<uint64_t>(nf * bs, n_samples - s0);
+                rc = fg::ctx_encode_chunk(c, (const uint8_t *)pcm + s0 * isz, ns, first_frame_number + f0,
+                                          &totals[r * n + i], frame_bytes ? frame_bytes + f0 : nullptr);
+                if (rc) rcs[i] = rc;
+            }
+            bar.wait();  // every total of round r (and every failure so far) is visible
+            bool any_fail = false;
+            for (uint64_t j = 0; j < n; j++) any_fail |= rcs[j] != FLACGPU_OK;
+            if (any_fail) return;  // all threads see the same flags after the barrier: all stop here
+            uint64_t off = 0;
+            for (uint64_t k = 0; k < r * n + i; k++) off += totals[k];
+            const uint64_t t = totals[r * n + i];
+            if (off + t > out_cap) {
+                rcs[i] = FLACGPU_ERR_OUTPUT_TOO_SMALL;
+            } else if (t) {
+                rc = fg::ctx_download_chunk(c, out + off, t);
+                if (rc) rcs[i] = rc;
+            }
         }
-    }
+    };
+    // threads wait at a gate until all exist: if one cannot be created, the others are
+    // released with "abort" before any of them reaches the barrier (which counts n)
+    std::mutex gm;
+    std::condition_variable gcv;
+    int gate = 0;  // 0 closed, 1 go, -1 abort
+    auto run = [&](uint64_t i) {
+        {
+            std::unique_lock<std::mutex> lk(gm);
+            gcv.wait(lk, [&] { return gate != 0; });
+            if (gate < 0) return;
+        }
+        work(i);
+    };
     std::vector<std::thread> th;
-    for (uint64_t i = 0; i < n; i++) {
-        if (parts[i].nf == 0) continue;
-        const uint64_t s0 = parts[i].f0 * bs, ns = std::min<uint64_t>(parts[i].nf * bs, n_samples - s0);
-        th.emplace_back([&, i, s0, ns]() {
-            Part &q = parts[i];
-            q.rc = flacgpu_encode_frames(m->ctx[i], (const uint8_t *)pcm + s0 * isz, bytes_per_sample, ns,
-                                         first_frame_number + q.f0, q.buf.data(), q.buf.size(), &q.len,
-                                         frame_bytes ? frame_bytes + q.f0 : nullptr);
-        });
+    int rc = FLACGPU_OK;
+    try {
+        th.reserve(n);
+        for (uint64_t i = 1; i < n; i++) th.emplace_back(run, i);
+    } catch (...) {
+        rc = FLACGPU_ERR_OUT_OF_MEMORY;
     }
+    {
+        std::lock_guard<std::mutex> lk(gm);
+        gate = rc ? -1 : 1;
+    }
+    gcv.notify_all();
+    if (!rc) work(0);
     for (std::thread &t : th) t.join();
-    size_t written = 0;
-    for (const Part &p : parts) {
-        if (p.rc) return p.rc;
-        if (written + p.len > out_cap) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
-        if (p.len) std::memcpy(out + written, p.buf.data(), p.len);
-        written += p.len;
-    }
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; i++)
+        if (rcs[i]) return rcs[i];
+    uint64_t written = 0;
+    for (uint64_t t : totals) written += t;
+    for (flacgpu_ctx *c : m->ctx) fg::ctx_finish(c);
     *out_len = written;
     return FLACGPU_OK;
 }
+
+}  // extern "C"

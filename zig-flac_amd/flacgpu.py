@@ -28,6 +28,7 @@ ERRORS = {
 }
 
 K_ANALYZE, K_ANALYZE_TAIL, K_SCAN, K_PACK, K_MD5 = range(5)
+MD5_HOST, MD5_DEVICE = 0, 1
 KERNEL_NAMES = ["analyze", "analyze_tail", "scan", "pack", "md5"]
 
 
@@ -85,6 +86,19 @@ class FrameRecord(ctypes.Structure):
         ("pad", ctypes.c_uint32),
         ("cand", SubframeRecord * 8),
     ]
+
+
+class Md5State(ctypes.Structure):
+    """flacgpu_md5_state: one stream's MD5 chaining value carried across calls."""
+    _fields_ = [("h", ctypes.c_uint32 * 4), ("bytes", ctypes.c_uint64), ("finished", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+def md5_states(n: int) -> bytes:
+    """n freshly initialised flacgpu_md5_state records (32 bytes each), ready to upload."""
+    arr = (Md5State * max(n, 1))()
+    load_library().flacgpu_md5_state_init(arr, n)
+    return bytes(arr)[: 32 * n]
 
 
 class WavInfo(ctypes.Structure):
@@ -172,6 +186,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_md5_update": (I32, [P, P, SZ]),
         "flacgpu_md5_final": (I32, [P, P]),
         "flacgpu_plan_create": (I32, [P, U32, P, P, U32, ctypes.POINTER(P)]),
+        "flacgpu_plan_create_segments": (I32, [P, U32, P, P, U32, P, P, ctypes.POINTER(P)]),
+        "flacgpu_plan_advance": (I32, [P, U64, P]),
+        "flacgpu_encode_plan_device_ex": (I32, [P, P, P, P, U64, P, P, P, P, P, P, P]),
+        "flacgpu_sync_check": (I32, [P, P]),
+        "flacgpu_md5_set_engine": (I32, [P, I32]),
+        "flacgpu_md5_get_engine": (I32, [P]),
+        "flacgpu_md5_state_init": (None, [P, SZ]),
         "flacgpu_plan_destroy": (None, [P]),
         "flacgpu_plan_frames": (U64, [P]),
         "flacgpu_plan_out_bound": (U64, [P]),
@@ -211,6 +232,8 @@ def exported_symbols() -> list:
         "flacgpu_encode_frame_planar", "flacgpu_md5_init", "flacgpu_md5_update", "flacgpu_md5_final",
         "flacgpu_plan_create", "flacgpu_plan_destroy", "flacgpu_plan_frames", "flacgpu_plan_out_bound",
         "flacgpu_plan_stream_first_frame", "flacgpu_encode_plan_device", "flacgpu_encode_plan_device_md5_async",
+        "flacgpu_plan_create_segments", "flacgpu_plan_advance", "flacgpu_encode_plan_device_ex", "flacgpu_sync_check",
+        "flacgpu_md5_set_engine", "flacgpu_md5_get_engine", "flacgpu_md5_state_init",
         "flacgpu_set_timing",
         "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_get_records",
         "flacgpu_get_config", "flacgpu_wav_parse", "flacgpu_streaminfo_init", "flacgpu_streaminfo_update_frame_size",
@@ -225,19 +248,28 @@ def _check(rc: int, where: str) -> None:
 
 
 class Plan:
-    def __init__(self, enc: "Encoder", offsets: Sequence[int], samples: Sequence[int]):
+    """flacgpu_plan: a batch of streams (or stream segments) laid out in one device PCM buffer."""
+
+    def __init__(self, enc: "Encoder", offsets: Sequence[int], samples: Sequence[int],
+                 first_frames: Optional[Sequence[int]] = None, final: Optional[Sequence[bool]] = None):
         self.enc = enc
         n = len(offsets)
         self._offs = (ctypes.c_uint64 * max(n, 1))(*offsets)
         self._samp = (ctypes.c_uint64 * max(n, 1))(*samples)
+        ff = (ctypes.c_uint64 * max(n, 1))(*first_frames) if first_frames is not None else None
+        fin = (ctypes.c_uint8 * max(n, 1))(*[1 if f else 0 for f in final]) if final is not None else None
         h = ctypes.c_void_p()
-        _check(enc.lib.flacgpu_plan_create(enc.ctx, n, self._offs, self._samp, enc.bytes_per_sample,
-                                           ctypes.byref(h)), "plan_create")
+        _check(enc.lib.flacgpu_plan_create_segments(enc.ctx, n, self._offs, self._samp, enc.bytes_per_sample, ff, fin,
+                                                    ctypes.byref(h)), "plan_create_segments")
         self.handle = h
         self.n_streams = n
         self.n_frames = enc.lib.flacgpu_plan_frames(h)
         self.out_bound = enc.lib.flacgpu_plan_out_bound(h)
         self.first_frame = [enc.lib.flacgpu_plan_stream_first_frame(h, s) for s in range(n)]
+
+    def advance(self, frames: int, stream: Optional[int] = None) -> None:
+        """flacgpu_plan_advance: the next window of the same streams (frame numbers + frames)."""
+        _check(self.enc.lib.flacgpu_plan_advance(self.handle, frames, stream or None), "plan_advance")
 
     def close(self) -> None:
         if self.handle:
@@ -337,7 +369,10 @@ class Encoder:
                "encode_frame_planar")
         return out.raw[: fb.value]
 
-    # ---- MD5 (md5.zig) on the GPU
+    # ---- MD5 (md5.zig): the context's engine (host core by default, one GPU lane opt-in)
+    def set_md5_engine(self, engine: int) -> None:
+        _check(self.lib.flacgpu_md5_set_engine(self.ctx, engine), "md5_set_engine")
+
     def md5(self, data: bytes) -> bytes:
         _check(self.lib.flacgpu_md5_init(self.ctx), "md5_init")
         buf = ctypes.create_string_buffer(bytes(data), len(data))
@@ -356,8 +391,43 @@ class Encoder:
         return d.raw
 
     # ---- device-resident batches
-    def plan(self, offsets: Sequence[int], samples: Sequence[int]) -> Plan:
-        return Plan(self, offsets, samples)
+    def plan(self, offsets: Sequence[int], samples: Sequence[int], first_frames: Optional[Sequence[int]] = None,
+             final: Optional[Sequence[bool]] = None) -> Plan:
+        return Plan(self, offsets, samples, first_frames, final)
+
+    def encode_plan_device_ex(self, plan: Plan, d_pcm: int, d_out: int, out_cap: int, d_frame_bytes: int,
+                              d_frame_offsets: int, d_total: int, d_md5_state: Optional[int] = None,
+                              d_md5: Optional[int] = None, stream: Optional[int] = None,
+                              md5_stream: Optional[int] = None) -> None:
+        """flacgpu_encode_plan_device_ex: MD5 state carried in d_md5_state (32 B per stream)."""
+        _check(self.lib.flacgpu_encode_plan_device_ex(
+            self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total,
+            d_md5_state or None, d_md5 or None, stream or None, md5_stream or None), "encode_plan_device_ex")
+
+    def sync_check(self, stream: Optional[int] = None) -> None:
+        """Synchronise `stream` and raise if a kernel flagged a device-side error."""
+        _check(self.lib.flacgpu_sync_check(self.ctx, stream or None), "sync_check")
+
+    def encode_frames_device(self, d_pcm: int, n_samples: int, first_frame: int = 0, stream: Optional[int] = None):
+        """Frames of n_samples interleaved samples at device address d_pcm, numbered from first_frame, kept in
+        device memory: returns (torch uint8 tensor of the bitstream, torch int32 tensor of frame sizes)."""
+        import torch
+
+        dev = torch.device("cuda", torch.cuda.current_device())
+        plan = self.plan([0], [n_samples], first_frames=[first_frame])
+        try:
+            d_out = torch.empty(max(int(plan.out_bound), 1), dtype=torch.uint8, device=dev)
+            d_fb = torch.empty(max(int(plan.n_frames), 1), dtype=torch.int32, device=dev)
+            d_off = torch.empty(max(int(plan.n_frames), 1), dtype=torch.int64, device=dev)
+            d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
+            st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+            self.encode_plan_device_ex(plan, d_pcm, d_out.data_ptr(), int(plan.out_bound), d_fb.data_ptr(),
+                                       d_off.data_ptr(), d_tot.data_ptr(), stream=st)
+            self.sync_check(st)
+            total = int(d_tot[0].item())
+            return d_out[:total], d_fb[: int(plan.n_frames)]
+        finally:
+            plan.close()
 
     def encode_plan_device(self, plan: Plan, d_pcm: int, d_out: int, out_cap: int, d_frame_bytes: int,
                            d_frame_offsets: int, d_total: int, d_md5: Optional[int] = None,
