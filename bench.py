@@ -4,39 +4,52 @@
 metric : MSamples/s encoded (whole node), 44.1kHz/16-bit stereo, blocksize 4096
 unit   : 1 sample = one interchannel sample (STREAMINFO unit, metadata.zig:24)
 
-A "step" is one pass of the hot path over one batch: every 4096-sample block
-of S independent streams (8192 streams x 8 blocks = 65536 blocks per GPU by
-default, BASELINE config 2)
-goes through the gfx950 kernels of libflacgpu.so -- analysis (mid/side, wasted
-bits, fixed-order analysis, Rice search, subframe choice, exact frame sizes),
-frame-size scan, pack (bit packing, CRC-8/16, frames written at their final
-offsets: one contiguous bitstream per stream) -- and the MD5 of every stream's
-raw PCM is computed on the GPU concurrently.  Inputs are resident in
-HBM before the timed region; outputs stay in HBM.  The MD5 is sequential
-within a stream (one lane per stream), so its rate grows with the number of
-streams in flight: 8192 streams keep it under the encode.
+Workload (config 2).  S independent long streams (files) per GPU, encoded F
+4096-sample blocks of each per step (8192 streams x 8 blocks = 65536 blocks =
+1 GiB of PCM per step by default): the reference's per-file block loop
+(wav2flac.zig:66-97) run for S files at once.  A step is one pass of the hot
+path over its batch: analysis (mid/side, wasted bits, fixed-order analysis,
+Rice search, subframe choice, exact frame sizes), frame-size scan, pack (bit
+packing, CRC-8/16, frames at their final offsets) and the MD5 of every
+stream's PCM.  Streams continue from step to step: frame numbers move on by F
+(flacgpu_plan_advance) and every stream's MD5 state is carried on the device
+(flacgpu_encode_plan_device_ex), so step k's MD5 chains follow step k-1's; the
+MD5 runs on its own HIP stream beside the next step's encode.  PCM is resident
+in HBM before the timed region (the same bytes each step); outputs stay in HBM.
+
+After the timed region the output is PROVED, not assumed: the device error word
+is checked (flacgpu_sync_check), a sample of streams' last-step frames is
+compared byte for byte with the CPU restatement (oracle/, with the same frame
+numbers), and their carried MD5 states are finalised on the device and compared
+with hashlib over the bytes they absorbed.  `output_ok` is that comparison.
 
 One process per GPU (torchrun for N > 1).  Streams are independent files, so
 ranks shard streams with no data-path collective (weak scaling); a barrier and
 a max-over-ranks reduction bracket the timed region.
 
 The JSON line also carries:
-  roofline     -- the dominant kernel (analysis or pack, whichever takes
-                  longer): its algorithmic bytes per launch (analysis: PCM
-                  read; pack: PCM read + frame bytes written) / its mean launch
-                  time, measured with HIP events on the launch stream during
-                  the timed steps, against 8 TB/s; `traffic` from the
-                  committed rocprofv3 PMC profile (profiles/), else null;
-  cpu_baseline -- the CPU restatement (oracle/, "port") timed on host
-                  threads over a bounded sample of the same workload.
+  roofline      -- the dominant kernel (analysis, pack or MD5: the longest mean
+                   launch), its algorithmic bytes per launch / its mean launch time
+                   from HIP events on its stream, against 8 TB/s; `traffic` from the
+                   committed rocprofv3 PMC summary of the same workload and kernel
+                   (profiles/), else null; `limiter` = what DESIGN.md measures binds;
+  stream_curve  -- the same blocks per step at 8 .. 16384 concurrent streams: the
+                   per-stream MD5 chain is the Amdahl term (rank 0, N = 1);
+  end_to_end    -- BASELINE.md's host-buffer contract: 8 ten-minute WAV-sized PCM
+                   buffers in host memory -> .flac files in host memory (H2D,
+                   kernels, D2H, MD5 on host threads, 73-byte header) (rank 0, N = 1);
+  cpu_baseline  -- the CPU restatement (oracle/, "port", -O3) on P pinned host
+                   threads over a bounded sample of the same workload.
 """
 from __future__ import annotations
 
 import argparse
 import ctypes
 import glob
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import threading
 import time
@@ -48,6 +61,11 @@ METRIC = "MSamples/s encoded (whole node), 44.1kHz/16-bit stereo, blocksize 4096
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # BASELINE.json configs (channels, bits, rate, LPC max order); c2 is the headline metric's
 PRESETS = {"c2": (2, 16, 44100, 0), "c3": (2, 24, 96000, 8), "c4": (8, 24, 96000, 0), "c5": (2, 32, 192000, 12)}
+LIMITER = {  # what binds each kernel (measured, not the roofline it is priced on)
+    "analyze": "VALU issue/latency (integer dependent chains per lane), not HBM",
+    "pack": "LDS atomics + dependent bit-offset chains, not HBM",
+    "md5": "per-stream dependent-op latency: one lane per stream, 64 sequential steps per 64-B block",
+}
 
 
 def parse():
@@ -55,97 +73,364 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--frames", type=int, default=65536, help="4096-sample blocks per GPU")
-    p.add_argument("--streams", type=int, default=8192, help="independent streams (files) per GPU")
+    p.add_argument("--frames", type=int, default=65536, help="4096-sample blocks per GPU per step")
+    p.add_argument("--streams", type=int, default=8192, help="concurrent streams (files) per GPU")
+    p.add_argument("--config", choices=sorted(PRESETS), default=None,
+                   help="BASELINE.json config preset (overrides --channels/--bits/--rate/--lpc); default c2")
     p.add_argument("--channels", type=int, default=2)
     p.add_argument("--bits", type=int, default=16)
     p.add_argument("--rate", type=int, default=44100)
     p.add_argument("--lpc", type=int, default=0, help="LPC max order (0 = fixed prediction, the reference)")
-    p.add_argument("--config", choices=sorted(PRESETS), default=None,
-                   help="BASELINE.json config preset (overrides --channels/--bits/--rate/--lpc); default c2")
     p.add_argument("--no-md5", action="store_true", help="skip the per-stream GPU MD5 (diagnostics only)")
-    p.add_argument("--md5-join", action="store_true",
-                   help="join each step's MD5 back into the encode stream (no overlap of consecutive steps)")
-    p.add_argument("--stream-pad", type=int, default=0,
-                   help="bytes of gap between consecutive streams in HBM (multiple of 4; layout diagnostics)")
-    p.add_argument("--cpu-frames", type=int, default=32768, help="blocks in the CPU-baseline sample")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--verify-streams", type=int, default=64, help="streams compared with the oracle after timing")
+    p.add_argument("--no-curve", action="store_true")
+    p.add_argument("--curve", default="8,64,1024,8192,16384")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--e2e-files", type=int, default=8)
+    p.add_argument("--e2e-minutes", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--verify", action="store_true", help="decode + check a sample of streams after timing")
+    p.add_argument("--cpu-frames", type=int, default=98304, help="blocks in the CPU-baseline sample")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0: the CPU share (OMP_NUM_THREADS), capped at a socket")
     a = p.parse_args()
     if a.config:
         a.channels, a.bits, a.rate, a.lpc = PRESETS[a.config]
     return a
 
 
-def make_pool(n, ch, bits, rate):
-    import synth
-
-    return synth.synth_samples(n, ch, bits, rate, stream=0)
+def workload_key(a) -> str:
+    return f"{a.config or 'c2'}:{a.frames}x{a.streams}"
 
 
 def build_input(args, rank):
-    """Synthetic PCM for S streams: windows of a seeded pool (SURVEY.md 8(d) signal)."""
+    """S streams of F blocks, contiguous, cut from a seeded pool (SURVEY.md 8(d) signal mix)."""
     import numpy as np
     import synth
 
     S, F = args.streams, args.frames // args.streams
     ch, bits = args.channels, args.bits
     n_per = F * 4096
-    pool_n = max(8 * 4096 * 64, n_per + 4096 * 64)
-    pool = make_pool(pool_n, ch, bits, args.rate)
+    pool_n = max(8 * 4096 * 64, min(n_per, 4096 * 4096) + 4096 * 64)
+    pool = synth.synth_samples(pool_n, ch, bits, args.rate, stream=0)
     pcm_pool = np.frombuffer(synth.to_pcm_bytes(pool, bits), dtype=np.uint8)
     fb = ch * (bits // 8)
     rng = np.random.Generator(np.random.PCG64(20260821 + 7919 * rank))
-    starts = rng.integers(0, (pool_n - n_per) // 4096 + 1, size=S) * 4096
-    stream_bytes = n_per * fb
-    pitch = stream_bytes + args.stream_pad
-    buf = np.zeros(S * pitch, dtype=np.uint8)
+    buf = np.empty(args.frames * 4096 * fb, dtype=np.uint8)
+    blocks = (pool_n - 4096) // 4096
+    # each stream: a run of pool windows (4096-block windows at random starts)
     for s in range(S):
-        a = int(starts[s]) * fb
-        buf[s * pitch:s * pitch + stream_bytes] = pcm_pool[a:a + stream_bytes]
-    offsets = [s * pitch for s in range(S)]
-    samples = [n_per] * S
-    return buf, offsets, samples
+        done = 0
+        while done < n_per:
+            take = min(n_per - done, 4096 * 4096, (pool_n // 4096 - 1) * 4096)
+            a = int(rng.integers(0, blocks - take // 4096 + 1)) * 4096 * fb
+            o = (s * n_per + done) * fb
+            buf[o:o + take * fb] = pcm_pool[a:a + take * fb]
+            done += take
+    return buf
 
 
-def cpu_baseline(buf, offsets, samples, args):
-    """Oracle (scalar C restatement) on host threads over a bounded sample."""
+# ---------------------------------------------------------------------------------------------
+# the GPU step loop (one plan = S streams x F blocks at fixed device offsets)
+class Workload:
+    def __init__(self, enc, d_pcm, S, F, fb, dev, md5=True):
+        import flacgpu
+        import numpy as np
+        import torch
+
+        self.enc, self.S, self.F = enc, S, F
+        n_per = F * 4096
+        self.offsets = [s * n_per * fb for s in range(S)]
+        self.plan = enc.plan(self.offsets, [n_per] * S, first_frames=[0] * S, final=[False] * S)
+        self.d_pcm = d_pcm
+        self.out_cap = int(self.plan.out_bound)
+        self.d_out = torch.empty(self.out_cap, dtype=torch.uint8, device=dev)
+        self.d_fb = torch.empty(self.plan.n_frames, dtype=torch.int32, device=dev)
+        self.d_off = torch.empty(self.plan.n_frames, dtype=torch.int64, device=dev)
+        self.d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.d_state = torch.from_numpy(np.frombuffer(flacgpu.md5_states(S), dtype=np.uint8).copy()).to(dev)
+        self.md5 = md5
+        self.stream = torch.cuda.current_stream(dev)
+        self.md5_stream = torch.cuda.Stream(dev)  # in order: each stream's MD5 chain follows the last step's
+        self.steps_done = 0
+
+    def step(self):
+        if self.steps_done:
+            self.plan.advance(self.F, self.stream.cuda_stream)
+        self.enc.encode_plan_device_ex(self.plan, self.d_pcm.data_ptr(), self.d_out.data_ptr(), self.out_cap,
+                                       self.d_fb.data_ptr(), self.d_off.data_ptr(), self.d_tot.data_ptr(),
+                                       self.d_state.data_ptr() if self.md5 else None, None,
+                                       stream=self.stream.cuda_stream, md5_stream=self.md5_stream.cuda_stream)
+        self.steps_done += 1
+
+    def close(self):
+        self.plan.close()
+
+
+def run_timed(w, steps, warmup, dist=None):
+    import torch
+
+    for _ in range(warmup):
+        w.step()
+    torch.cuda.synchronize()
+    w.enc.reset_timing()
+    w.enc.set_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        w.step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    w.enc.set_timing(False)
+    return t1 - t0
+
+
+def verify(args, w, buf, fb, n_verify, dev):
+    """Last step's frames of a sample of streams == the oracle's; their carried MD5 == hashlib."""
+    import numpy as np
+    import torch
+
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref
 
-    L = oracle_ref.lib()
+    enc = w.enc
+    enc.sync_check(w.stream.cuda_stream)
+    enc.sync_check(w.md5_stream.cuda_stream)
+    total = int(w.d_tot[0].item())
+    sizes = w.d_fb.cpu().numpy()
+    offs = w.d_off.cpu().numpy()
+    ok = total == int(sizes.astype(np.int64).sum()) and total > 0
+    first_number = (w.steps_done - 1) * w.F
+    picks = sorted(set(int(x) for x in np.linspace(0, w.S - 1, min(n_verify, w.S))))
+    n_per = w.F * 4096
+    for s in picks:
+        f0 = w.plan.first_frame[s]
+        f1 = w.plan.first_frame[s + 1] if s + 1 < w.S else int(w.plan.n_frames)
+        a = int(offs[f0])
+        b = int(offs[f1]) if f1 < int(w.plan.n_frames) else total
+        pcm = bytes(buf[w.offsets[s]:w.offsets[s] + n_per * fb])
+        ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, args.channels, args.bits, args.rate, lpc=args.lpc,
+                                                     first_frame=first_number)
+        got = w.d_out[a:b].cpu().numpy().tobytes()
+        ok &= got == ref and [int(x) for x in sizes[f0:f1]] == ref_sizes
+    md5_ok = None
+    if w.md5:
+        # finalise every stream's carried state with an empty final segment, on the device
+        fin = enc.plan(w.offsets, [0] * w.S, final=[True] * w.S)
+        d_md5 = torch.zeros(16 * w.S, dtype=torch.uint8, device=dev)
+        d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
+        dummy = torch.zeros(16, dtype=torch.uint8, device=dev)
+        enc.encode_plan_device_ex(fin, w.d_pcm.data_ptr(), dummy.data_ptr(), 16, dummy.data_ptr(), dummy.data_ptr(),
+                                  d_tot.data_ptr(), w.d_state.data_ptr(), d_md5.data_ptr(),
+                                  stream=w.stream.cuda_stream)
+        enc.sync_check(w.stream.cuda_stream)
+        fin.close()
+        dig = d_md5.cpu().numpy().reshape(-1, 16)
+        md5_ok = True
+        for s in picks[:16]:
+            pcm = bytes(buf[w.offsets[s]:w.offsets[s] + n_per * fb])
+            h = hashlib.md5()
+            for _ in range(w.steps_done):
+                h.update(pcm)
+            md5_ok &= dig[s].tobytes() == h.digest()
+        ok &= md5_ok
+    return bool(ok), {"streams_compared": len(picks), "frame_numbers_from": first_number,
+                      "md5_streams_compared": min(16, len(picks)) if w.md5 else 0}
+
+
+def kernel_times(enc):
+    import flacgpu
+
+    return {name: enc.kernel_time(k) for k, name in enumerate(flacgpu.KERNEL_NAMES)}
+
+
+def read_pmc(key, kernel):
+    """(HBM bytes per launch, counters) of `kernel` in the committed PMC summary of workload `key`."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("workload") != key:
+            continue
+        return (d.get("hbm_bytes_per_launch", {}).get(kernel),
+                d.get("counters_per_dispatch", {}).get(kernel, {}), os.path.basename(f))
+    return None, {}, None
+
+
+# ---------------------------------------------------------------------------------------------
+def stream_curve(args, enc, d_pcm, fb, dev):
+    """Same blocks per step at S concurrent streams: encode vs the per-stream MD5 chain."""
+    out = []
+    for S in [int(x) for x in args.curve.split(",") if x]:
+        if args.frames % S:
+            continue
+        F = args.frames // S
+        w = Workload(enc, d_pcm, S, F, fb, dev)
+        steps = 2 if F <= 64 else 1
+        dt = run_timed(w, steps, 1)
+        kt = kernel_times(enc)
+        per = {k: round(v[1] / v[0], 3) for k, v in kt.items() if v[0]}
+        samples = S * F * 4096 * steps
+        out.append({"streams": S, "blocks_per_stream_per_step": F, "value": round(samples / dt / 1e6, 1),
+                    "ms_per_step": round(dt / steps * 1e3, 3), "kernel_ms": per})
+        w.close()
+    return out
+
+
+def end_to_end(args):
+    """BASELINE.md end-to-end contract: host PCM buffers -> .flac files in host memory."""
+    import numpy as np
+    import flacgpu
+    import synth
+
+    ch, bits, rate = 2, 16, 44100
+    n = int(args.e2e_minutes * 60 * rate)
+    fb = ch * 2
+    pool_n = 4096 * 1024
+    pool = np.frombuffer(synth.to_pcm_bytes(synth.synth_samples(pool_n, ch, bits, rate, stream=11), bits),
+                         dtype=np.uint8)
+    files = []
+    for i in range(args.e2e_files):
+        buf = np.empty(n * fb, dtype=np.uint8)
+        pos, k = 0, i
+        while pos < n:
+            take = min(n - pos, pool_n - 4096 * (k % 64))
+            a = 4096 * (k % 64) * fb
+            buf[pos * fb:(pos + take) * fb] = pool[a:a + take * fb]
+            pos += take
+            k += 7
+        files.append(buf)
+    L = flacgpu.load_library()
+    encs = [flacgpu.Encoder(ch, bits, rate, device=0, max_frames=4096) for _ in files]
+    cap = 200 + ((n + 4095) // 4096 + 1) * encs[0].frame_bound()
+    outs = [np.empty(cap, dtype=np.uint8) for _ in files]
+    lens = [ctypes.c_size_t(0) for _ in files]
+    rcs = [0] * len(files)
+
+    def one(i):
+        rcs[i] = L.flacgpu_encode_file(encs[i].ctx, files[i].ctypes.data_as(ctypes.c_void_p), 2, n,
+                                       outs[i].ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(lens[i]))
+
+    def run_all():
+        th = [threading.Thread(target=one, args=(i,)) for i in range(len(files))]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return time.perf_counter() - t0
+
+    run_all()
+    best = min(run_all() for _ in range(2))
+    ok = all(r == 0 for r in rcs)
+    # parts, measured alone: one file's MD5 on one host core; all files' encodes without MD5
+    t0 = time.perf_counter()
+    hashlib.md5(files[0]).digest()
+    md5_s = time.perf_counter() - t0
+    frames_caps = [np.empty(cap, dtype=np.uint8) for _ in files]
+
+    def enc_only(i):
+        ol = ctypes.c_size_t(0)
+        L.flacgpu_encode_frames(encs[i].ctx, files[i].ctypes.data_as(ctypes.c_void_p), 2, n, 0,
+                                frames_caps[i].ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(ol), None)
+
+    th = [threading.Thread(target=enc_only, args=(i,)) for i in range(len(files))]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    enc_s = time.perf_counter() - t0
+    # proof: file 0 is byte-identical to the restatement's whole-file encode (header, MD5, frames)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref
+
+    ref = oracle_ref.encode_file(files[0].tobytes(), ch, bits, rate)
+    ok &= outs[0][: lens[0].value].tobytes() == ref
+    for e in encs:
+        e.close()
+    total = n * len(files)
+    return {"files": len(files), "minutes_per_file": args.e2e_minutes, "samples": total,
+            "value": round(total / best / 1e6, 1), "unit": "MSamples/s", "wall_ms": round(best * 1e3, 2),
+            "md5_one_file_host_core_ms": round(md5_s * 1e3, 2), "encode_only_all_files_ms": round(enc_s * 1e3, 2),
+            "path": "pageable host PCM -> flacgpu_encode_file per file (one context + host thread each): "
+                    "H2D, kernels, D2H pipelined in 2048-frame chunks; MD5 on a host thread per file beside "
+                    "the encode; 73-byte header + frames in host memory",
+            "output_ok": bool(ok)}
+
+
+# ---------------------------------------------------------------------------------------------
+def cpu_facts():
+    facts = {"model": None, "cores_per_socket": None, "sockets": None}
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True).stdout.splitlines():
+            k, _, v = line.partition(":")
+            v = v.strip()
+            if k == "Model name":
+                facts["model"] = v
+            elif k == "Core(s) per socket":
+                facts["cores_per_socket"] = int(v)
+            elif k == "Socket(s)":
+                facts["sockets"] = int(v)
+    except Exception:
+        pass
+    return facts
+
+
+def socket0_cpus():
+    try:
+        txt = open("/sys/devices/system/node/node0/cpulist").read().strip()
+        cpus = []
+        for part in txt.split(","):
+            a, _, b = part.partition("-")
+            cpus += list(range(int(a), int(b or a) + 1))
+        avail = os.sched_getaffinity(0)
+        return [c for c in cpus if c in avail]
+    except Exception:
+        return sorted(os.sched_getaffinity(0))
+
+
+def cpu_baseline(buf, args):
+    """The CPU restatement (oracle/, built -O3 -march=x86-64-v4 as liboracle_fast.so) on P
+    threads pinned to distinct cores of socket 0, each encoding whole streams (incl. MD5)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref
+
+    L = oracle_ref.lib(fast=True)
+    facts = cpu_facts()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    P = args.cpu_threads or min(share, facts["cores_per_socket"] or share)
+    cpus = socket0_cpus()
     ch, bits = args.channels, args.bits
     fb = ch * (bits // 8)
-    # each thread encodes whole streams (thread t: streams t, t+T, ...) until it has its share of blocks
-    per_thread = max(1, args.cpu_frames // args.cpu_threads)
-    jobs = []
-    for t in range(args.cpu_threads):
-        mine, blocks, s = [], 0, t
-        while blocks < per_thread and s < len(offsets):
-            nb = (samples[s] + 4095) // 4096
-            mine.append(bytes(buf[offsets[s]:offsets[s] + samples[s] * fb]))
-            blocks += nb
-            s += args.cpu_threads
-        jobs.append(mine)
+    per_stream = 8 * 4096  # 8-block streams, the headline's shape
+    n_streams_buf = len(buf) // (per_stream * fb)
+    per_thread = max(1, args.cpu_frames // P // 8)
     cfg = oracle_ref.config(ch, bits, args.rate, lpc=args.lpc)
-    res = [0] * len(jobs)
+    res = [0] * P
+    cap = 8 * L.oracle_max_frame_bytes(4096, bits, ch) + 64
 
-    def run(i):
+    def run(t):
+        try:
+            os.sched_setaffinity(0, {cpus[t % len(cpus)]})  # this thread only
+        except Exception:
+            pass
+        out = ctypes.create_string_buffer(cap)
+        sizes = (ctypes.c_uint32 * 8)()
+        md5 = ctypes.create_string_buffer(16)
         done = 0
-        for pcm in jobs[i]:
-            n = len(pcm) // fb
-            nf = (n + 4095) // 4096
-            cap = nf * L.oracle_max_frame_bytes(4096, bits, ch) + 64
-            out = ctypes.create_string_buffer(cap)
-            sizes = (ctypes.c_uint32 * nf)()
-            md5 = ctypes.create_string_buffer(16)
-            r = L.oracle_encode_stream(ctypes.byref(cfg), pcm, bits // 8, ctypes.c_uint64(n), ctypes.c_uint64(0),
-                                       out, ctypes.c_size_t(cap), sizes, md5)
-            done += n if r > 0 else 0
-        res[i] = done
+        for j in range(per_thread):
+            s = (t + j * P) % n_streams_buf
+            base = buf.ctypes.data + s * per_stream * fb
+            r = L.oracle_encode_stream(ctypes.byref(cfg), ctypes.c_void_p(base), bits // 8, ctypes.c_uint64(per_stream),
+                                       ctypes.c_uint64(0), out, ctypes.c_size_t(cap), sizes, md5)
+            done += per_stream if r > 0 else 0
+        res[t] = done
 
-    th = [threading.Thread(target=run, args=(i,)) for i in range(len(jobs))]
+    th = [threading.Thread(target=run, args=(t,)) for t in range(P)]
     t0 = time.perf_counter()
     for t in th:
         t.start()
@@ -153,53 +438,28 @@ def cpu_baseline(buf, offsets, samples, args):
         t.join()
     dt = time.perf_counter() - t0
     tot = sum(res)
+    value = tot / dt / 1e6
+    cps = facts["cores_per_socket"]
     return {
-        "value": round(tot / dt / 1e6, 3),
+        "value": round(value, 3),
         "unit": "MSamples/s",
-        "cores": args.cpu_threads,
+        "cores": P,
         "kind": "port",
-        "sample": f"{tot} samples ({sum(len(j) for j in jobs)} whole streams, {tot // 4096} blocks, incl. MD5) on "
-                  f"{args.cpu_threads} host threads (one oracle encode per stream), {dt:.2f}s wall",
+        "sample": f"{tot} samples ({tot // 4096} blocks as {P * per_thread} 8-block streams, incl. MD5), "
+                  f"{P} threads pinned to socket-0 cores, {dt:.2f}s wall ({dt * P:.1f} CPU-s)",
+        "cpu_model": facts["model"],
+        "cores_per_socket": cps,
+        "sockets": facts["sockets"],
+        "build": "oracle/flac_oracle.c -O3 -march=x86-64-v4 (scalar C restatement; the Zig reference is "
+                 "unbuildable here: no Zig 0.16 on the box)",
+        "per_core": round(value / P, 3),
+        "single_socket_estimate": round(value / P * cps, 1) if cps else None,
+        "single_socket_note": f"P = {P} (the box's CPU share for one GPU) of {cps} cores per socket were run; "
+                              "the socket figure scales the measured per-core rate linearly (an upper bound)",
     }
 
 
-def read_traffic(kernel, frames_per_launch):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (profiles/*pmc*.json)."""
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    if not cands:
-        return None
-    try:
-        d = json.load(open(cands[-1]))
-        if d.get("frames_per_launch") != frames_per_launch:
-            return None
-        return d.get("hbm_bytes_per_launch", {}).get(kernel)
-    except Exception:
-        return None
-
-
-def read_issue(kernel, frames_per_launch, avg_s):
-    """VALU issue load of `kernel` from the committed PMC summary: wave-instructions per launch
-    against 1024 SIMDs x 0.5 wave64 VALU instructions/clock (SIMD-32, 2 passes; MI355X_MICROARCH.md)
-    at 2.4 GHz.  A lower bound on VALU busy (64-bit and transcendental ops take more passes)."""
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    if not cands or avg_s <= 0:
-        return None
-    try:
-        d = json.load(open(cands[-1]))
-        if d.get("frames_per_launch") != frames_per_launch:
-            return None
-        c = d.get("counters_per_dispatch", {}).get(kernel, {})
-        valu, salu = c.get("SQ_INSTS_VALU"), c.get("SQ_INSTS_SALU")
-        if not valu:
-            return None
-        peak = 1024 * 0.5 * 2.4e9
-        return {"valu_wave_instr_per_launch": valu, "salu_wave_instr_per_launch": salu,
-                "peak_valu_wave_instr_per_s": peak, "valu_issue_frac": round(valu / avg_s / peak, 4),
-                "source": os.path.basename(cands[-1])}
-    except Exception:
-        return None
-
-
+# ---------------------------------------------------------------------------------------------
 def main():
     args = parse()
     import numpy as np
@@ -223,98 +483,58 @@ def main():
 
     if args.frames % args.streams:
         raise SystemExit("--frames must be a multiple of --streams")
-    buf, offsets, samples = build_input(args, rank)
+    buf = build_input(args, rank)
+    fb = args.channels * (args.bits // 8)
     enc = flacgpu.Encoder(args.channels, args.bits, args.rate, device=torch.cuda.current_device(),
                           max_frames=args.frames, lpc_order=args.lpc)
-    plan = enc.plan(offsets, samples)
     d_pcm = torch.from_numpy(buf).to(dev)
-    out_cap = int(plan.out_bound)
-    d_out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
-    d_fb = torch.empty(plan.n_frames, dtype=torch.int32, device=dev)
-    d_off = torch.empty(plan.n_frames, dtype=torch.int64, device=dev)
-    d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
-    d_md5 = torch.zeros(args.streams * 16, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    # The MD5 is per-stream sequential (latency-bound), the encode throughput-bound: step k's MD5
-    # runs on its own HIP stream (two alternate) and overlaps step k+1's encode.  Every step's MD5
-    # and frames are complete at the synchronize that closes the timed region.
-    md5_streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-    n_step = [0]
-
-    def step():
-        ms = None if args.md5_join else md5_streams[n_step[0] % 2].cuda_stream
-        n_step[0] += 1
-        enc.encode_plan_device(plan, d_pcm.data_ptr(), d_out.data_ptr(), out_cap, d_fb.data_ptr(),
-                               d_off.data_ptr(), d_tot.data_ptr(), None if args.no_md5 else d_md5.data_ptr(),
-                               stream.cuda_stream, md5_stream=ms)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    enc.reset_timing()
-    enc.set_timing(True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    enc.set_timing(False)
-    elapsed = t1 - t0
+    F = args.frames // args.streams
+    w = Workload(enc, d_pcm, args.streams, F, fb, dev, md5=not args.no_md5)
+    elapsed = run_timed(w, args.steps, args.warmup, dist)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    samples_per_rank = sum(samples)
+    samples_per_rank = args.frames * 4096
     value = samples_per_rank * world * args.steps / elapsed / 1e6
 
     # roofline of the dominant kernel, from HIP events on its stream
-    kt = {name: enc.kernel_time(k) for k, name in enumerate(flacgpu.KERNEL_NAMES)}
-    fb = d_fb.cpu().numpy().astype(np.int64)
-    total_bytes = int(d_tot[0].item())
-    frame_in = 4096 * args.channels * (args.bits // 8)
-    n_frames = int(plan.n_frames)
+    kt = kernel_times(enc)
+    fbytes = w.d_fb.cpu().numpy().astype(np.int64)
+    total_bytes = int(w.d_tot[0].item())
+    pcm_bytes = args.frames * 4096 * fb
     per_launch = {name: (v[1] / v[0]) / 1e3 for name, v in kt.items() if v[0]}
-    dom = "pack" if per_launch.get("pack", 0) > per_launch.get("analyze", 0) else "analyze"
-    algo_bytes = n_frames * frame_in + (int(fb.sum()) if dom == "pack" else 0)
-    n_launch = kt[dom][0]
-    avg_s = per_launch.get(dom, 0.0)
-    achieved = algo_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic = read_traffic(dom, n_frames)
+    cands = [k for k in ("analyze", "pack", "md5") if k in per_launch]
+    dom = max(cands, key=lambda k: per_launch[k])
+    algo_bytes = pcm_bytes + (int(fbytes.sum()) if dom == "pack" else 0)
+    avg_s = per_launch[dom]
+    achieved = algo_bytes / avg_s / 1e9
+    key = workload_key(args)
+    traffic, counters, pmc_src = read_pmc(key, dom)
+    issue = None
+    if counters.get("SQ_INSTS_VALU"):
+        peak = 1024 * 0.5 * 2.4e9  # wave64 VALU instructions/s: 1024 SIMDs x 1 per 2 cycles x 2.4 GHz
+        issue = {"valu_wave_instr_per_launch": counters["SQ_INSTS_VALU"], "peak_valu_wave_instr_per_s": peak,
+                 "valu_issue_frac": round(counters["SQ_INSTS_VALU"] / avg_s / peak, 4),
+                 "waves_per_launch": counters.get("SQ_WAVES"), "source": pmc_src}
     path_s = sum(per_launch.get(k, 0.0) for k in ("analyze", "analyze_tail", "scan", "pack"))
-    path_bytes = n_frames * frame_in + int(fb.sum())
 
-    # validity checks on the last step's output
-    ok = bool(total_bytes == int(fb.sum()) and total_bytes > 0)
-    if args.verify and rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import hashlib
-        import oracle_ref
+    ok, vinfo = verify(args, w, buf, fb, args.verify_streams, dev) if rank == 0 else (True, {})
+    w.close()
 
-        out = d_out[:total_bytes].cpu().numpy().tobytes()
-        offs = d_off.cpu().numpy()
-        md5s = d_md5.cpu().numpy().reshape(-1, 16)
-        for s in list(range(0, args.streams, max(1, args.streams // 8))):
-            f0 = plan.first_frame[s]
-            f1 = plan.first_frame[s + 1] if s + 1 < args.streams else plan.n_frames
-            a = int(offs[f0])
-            b = int(offs[f1]) if f1 < plan.n_frames else total_bytes
-            pcm = bytes(buf[offsets[s]:offsets[s] + samples[s] * frame_in // 4096])
-            dec, _ = oracle_ref.decode_frames(out[a:b], args.channels, args.bits, args.rate, samples[s])
-            ok &= dec == pcm
-            if not args.no_md5:
-                ok &= md5s[s].tobytes() == hashlib.md5(pcm).digest()
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(buf, offsets, samples, args)
+    curve = e2e = cpu = None
+    if rank == 0 and world == 1:
+        if not args.no_curve and not args.no_md5:
+            curve = stream_curve(args, enc, d_pcm, fb, dev)
+        if not args.no_e2e and (args.config or "c2") == "c2":
+            del d_pcm
+            torch.cuda.empty_cache()
+            e2e = end_to_end(args)
+        if not args.no_cpu:
+            cpu = cpu_baseline(buf, args)
 
     if rank == 0:
+        cfg = (args.config or "c2").upper()
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -329,40 +549,45 @@ def main():
             "dtype": "int32",
             "data": "synthetic",
             "config": {
-                "workload": f"{(args.config or 'c2').upper()}: {args.rate/1000:g}kHz {args.bits}-bit "
-                            f"{args.channels}ch, blocksize 4096, "
-                            f"{args.frames} blocks/GPU as {args.streams} streams x {args.frames // args.streams} "
-                            f"blocks, " + (f"LPC orders 1..{args.lpc} + full subframe-type search"
-                                           if args.lpc else "fixed prediction") +
-                            f", per-stream GPU MD5" + (" (off)" if args.no_md5 else
-                                                          (" joined per step" if args.md5_join else
-                                                           " overlapping the next step's encode")),
-                "blocks_per_gpu": args.frames,
+                "workload": f"{cfg}: {args.rate/1000:g}kHz {args.bits}-bit {args.channels}ch, blocksize 4096, "
+                            f"{args.streams} concurrent streams/GPU x {F} blocks each per step "
+                            f"({args.frames} blocks/step), frame numbers + per-stream MD5 state carried across "
+                            "steps, " + (f"LPC orders 1..{args.lpc} + full subframe-type search"
+                                         if args.lpc else "fixed prediction") +
+                            (", MD5 off (diagnostic)" if args.no_md5 else
+                             ", MD5 on its own HIP stream beside the next step's encode"),
+                "workload_key": key,
+                "blocks_per_gpu_per_step": args.frames,
                 "streams_per_gpu": args.streams,
-                "samples_per_gpu": samples_per_rank,
-                "compression_ratio": round(total_bytes / (samples_per_rank * frame_in / 4096), 4),
+                "samples_per_gpu_per_step": samples_per_rank,
+                "compression_ratio": round(total_bytes / pcm_bytes, 4),
                 "parallelism": f"streams sharded over {world} GPU(s), no collective on the data path",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_analyze (4096-sample frames)" if dom == "analyze" else "k_pack",
+                "limiter": LIMITER[dom],
+                "kernel": {"analyze": "k_analyze (4096-sample frames)", "pack": "k_pack4 / k_pack",
+                           "md5": "k_md5_streams"}[dom],
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
+                "traffic_source": pmc_src,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "avg_launch_ms": round(avg_s * 1e3, 4),
-                "launches": n_launch,
-                "encode_path_gbs": round(path_bytes / path_s / 1e9, 2) if path_s > 0 else None,
-                "issue": read_issue(dom, n_frames, avg_s),
+                "launches": kt[dom][0],
+                "encode_path_gbs": round((pcm_bytes + int(fbytes.sum())) / path_s / 1e9, 2) if path_s > 0 else None,
+                "issue": issue,
             },
             "kernel_ms_per_step": {k: round(v[1] / max(v[0], 1), 4) for k, v in kt.items() if v[0]},
             "output_ok": ok,
+            "verified": vinfo,
+            "stream_curve": curve,
+            "end_to_end": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    plan.close()
     enc.close()
     if dist:
         dist.destroy_process_group()

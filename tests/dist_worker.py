@@ -35,6 +35,7 @@ def main():
     p.add_argument("--rate", type=int, default=44100)
     p.add_argument("--samples", type=int, default=10 * 4096 + 123)
     p.add_argument("--md5", default="host")
+    p.add_argument("--backend", choices=["gloo", "nccl"], default="gloo")
     p.add_argument("--out", required=True)
     a = p.parse_args()
     import torch.distributed as dist
@@ -42,15 +43,25 @@ def main():
     import parallel
     import synth
 
-    dist.init_process_group("gloo")
+    import torch
+
     pcm = synth.synth_pcm(a.samples, a.channels, a.bits, a.rate)
+    if a.backend == "nccl":  # RCCL: one GPU per rank
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        device = f"cuda:{local}"
+    else:
+        dist.init_process_group("gloo")
+        device = "cpu"
     if a.encoder == "gpu":
         import flacgpu
 
-        enc = flacgpu.Encoder(a.channels, a.bits, a.rate, device=0, max_frames=256)
+        enc = flacgpu.Encoder(a.channels, a.bits, a.rate, device=torch.cuda.current_device() if a.backend == "nccl"
+                              else 0, max_frames=256)
     else:
         enc = OracleFrames(a.channels, a.bits, a.rate)
-    out = parallel.encode_sharded(enc, pcm, dist=dist, device="cpu", md5=a.md5)
+    out = parallel.encode_sharded(enc, pcm, dist=dist, device=device, md5=a.md5)
     if dist.get_rank() == 0:
         open(a.out, "wb").write(out)
     dist.barrier()

@@ -9,6 +9,7 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+LIB_FAST = os.path.join(ROOT, "oracle", "build", "liboracle_fast.so")  # -O3 build: bench.py cpu_baseline only
 
 
 class OConfig(ctypes.Structure):
@@ -34,10 +35,20 @@ class ORec(ctypes.Structure):
 
 
 _L = None
+_LF = None
 
 
-def lib():
-    global _L
+def lib(fast: bool = False):
+    global _L, _LF
+    if fast:
+        if _LF is None:
+            if not os.path.exists(LIB_FAST):
+                import subprocess
+                subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+            _LF = ctypes.CDLL(LIB_FAST)
+            _LF.oracle_encode_stream.restype = ctypes.c_long
+            _LF.oracle_max_frame_bytes.restype = ctypes.c_size_t
+        return _LF
     if _L is None:
         if not os.path.exists(LIB):
             import subprocess

@@ -118,6 +118,41 @@ def test_gpu_encode_file_matches_oracle(ch, bits, rate, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("block", [1152, 4096, 192, 4000])
+def test_gpu_encode_file_block_sizes(block):
+    """STREAMINFO min/max block size follows the context's block size (the reference only
+    runs 4096, wav_reader.zig:106-107, where both agree)."""
+    ch, bits, rate = 2, 16, 44100
+    n = 7 * block + 321
+    pcm = synth.synth_pcm(n, ch, bits, rate)
+    with flacgpu.Encoder(ch, bits, rate, max_frames=16, block_size=block) as enc:
+        out = enc.encode_file(pcm)
+    ref = oracle_ref.encode_file(pcm, ch, bits, rate, block=block)
+    assert out == ref
+    assert int.from_bytes(out[8:10], "big") == int.from_bytes(out[10:12], "big") == block
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", ["host", "device"])
+@pytest.mark.parametrize("n", [0, 1, 3 * 4096 + 1000, 40 * 4096])
+def test_md5_engines_match_hashlib(engine, n):
+    """flacgpu_md5_*: the default host engine and the opt-in one-GPU-lane engine, fed in
+    uneven pieces (Md5.update per block, wav_reader.zig:66), and encode_file with either."""
+    ch, bits, rate = 2, 16, 44100
+    pcm = synth.synth_pcm(n, ch, bits, rate) if n else b""
+    with flacgpu.Encoder(ch, bits, rate, max_frames=16) as enc:
+        if engine == "device":
+            enc.set_md5_engine(flacgpu.MD5_DEVICE)
+        assert enc.lib.flacgpu_md5_get_engine(enc.ctx) == (1 if engine == "device" else 0)
+        enc.lib.flacgpu_md5_init(enc.ctx)
+        for a in range(0, len(pcm), 1000 * 4 + 12):
+            enc.md5_update(pcm[a:a + 1000 * 4 + 12])
+        assert enc.md5_final() == hashlib.md5(pcm).digest()
+        out = enc.encode_file(pcm)
+    assert out == oracle_ref.encode_file(pcm, ch, bits, rate)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (2, 24, 96000), (1, 32, 48000)])
 def test_gpu_wav_to_flac(ch, bits, rate):
     n = 2 * 4096 + 77

@@ -7,7 +7,7 @@ are kilobytes (x1024); on gfx950 FETCH_SIZE counts half the bytes of wide
 coalesced reads, so it is doubled.  Counters are averaged per dispatch of each
 kernel family.
 
-Usage: tools/pmc_summary.py <prof_dir> <tag> <frames_per_launch>
+Usage: tools/pmc_summary.py <prof_dir> <tag> <frames_per_launch> <workload key (bench.py workload_key)>
 """
 import csv
 import json
@@ -30,6 +30,7 @@ def family(name):
 
 def main():
     d, tag, frames = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    workload = sys.argv[4] if len(sys.argv) > 4 else None
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stats = {}
     ks = os.path.join(d, "kt", "kt_kernel_stats.csv")
@@ -53,12 +54,12 @@ def main():
     for fam, cs in avg.items():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             hbm[fam] = round(cs["FETCH_SIZE"] * 1024 * 2 + cs["WRITE_SIZE"] * 1024)
-    out = {"tag": tag, "frames_per_launch": frames, "hbm_bytes_per_launch": hbm,
+    out = {"tag": tag, "workload": workload, "frames_per_launch": frames, "hbm_bytes_per_launch": hbm,
            "fetch_note": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count correction) + WRITE_SIZE KiB x1024",
            "kernel_stats": stats, "counters_per_dispatch": avg}
     os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
     json.dump(out, open(os.path.join(root, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
-    lines = [f"# rocprofv3 summary: {tag}", "", f"frames per launch: {frames}", "",
+    lines = [f"# rocprofv3 summary: {tag}", "", f"workload: {workload}; frames per launch: {frames}", "",
              "| kernel | calls | avg us | % time | HBM MB/launch (corrected) |", "|---|---|---|---|---|"]
     for fam in dict.fromkeys(f for f, _ in FAMILIES if f in stats):
         s = stats[fam]

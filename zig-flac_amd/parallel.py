@@ -3,16 +3,23 @@
 Frame f of a stream depends only on samples [f*B, f*B + n) and on f itself (the
 UTF-8 frame number, frame_writer.zig:235-251), so rank r of W encodes the
 contiguous frame range shard_frames(...) with its own GPU and numbers its frames
-from the range start.  The only exchange is the gather of the per-rank
-bitstreams and per-frame sizes to the rank that writes the file (SURVEY.md
-section 8e): an all-gather of (bytes, frames) counts, then point-to-point
-transfers of the variable-length pieces (RCCL over xGMI with backend "nccl",
-gloo in the CPU tests).  Rank 0 then replays updateFrameSize in frame order
-(metadata.zig:35-40) and writes the 73-byte header (encoder.zig:177-226).
+from the range start (the block loop of wav2flac.zig:66-97, cut into W pieces).
+The only exchange is the gather of the per-rank bitstreams and per-frame sizes
+to the rank that writes the file:
+
+  * each rank's frames stay where its encoder put them (device memory on a GPU:
+    flacgpu.Encoder.encode_frames_device, no host round trip);
+  * an all-gather of the (frames, bytes) counts, then point-to-point transfers
+    straight into slices of ONE receive buffer on rank 0, so the whole bitstream
+    arrives contiguous and in frame order (RCCL over xGMI with backend "nccl";
+    gloo moves the same tensors between CPU processes in the tests);
+  * rank 0 replays updateFrameSize in frame order (metadata.zig:35-40), copies the
+    bitstream to the host once and writes the 73-byte header (encoder.zig:177-226).
 
 The stream MD5 is sequential over the whole stream and does not shard: rank 0
-computes it (md5="gpu": the context's streaming GPU MD5; md5="host": a host
-thread overlapping the encode, the Amdahl term of SURVEY.md section 8e).
+computes it on a host thread that overlaps the encode and the gather (md5="host",
+the Amdahl term of SURVEY.md section 8e), or with the context's opt-in GPU lane
+(md5="gpu").
 """
 from __future__ import annotations
 
@@ -31,39 +38,75 @@ def shard_frames(n_samples: int, block: int, world: int, rank: int) -> Tuple[int
     return f0, f0 + base + (1 if rank < extra else 0)
 
 
-def _gather_bytes(dist, group, payload: bytes, device, rank: int, world: int):
-    """Rank 0 receives every rank's payload (variable length); returns the list on rank 0."""
+def gather_frames(dist, group, frames, sizes, rank: int, world: int):
+    """Gather every rank's (bitstream, frame sizes) tensors to rank 0.
+
+    frames: uint8 tensor, sizes: int32 tensor, both on this rank's communication
+    device.  Rank 0 gets (one uint8 tensor holding all ranks' bitstreams in rank
+    order, one int32 tensor of all frame sizes); other ranks get None.
+    """
     import torch
 
-    n = torch.tensor([len(payload)], dtype=torch.int64, device=device)
-    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    device = frames.device
+    counts = torch.tensor([sizes.numel(), frames.numel()], dtype=torch.int64, device=device)
+    allc = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(allc, counts, group=group)
+    nfr = [int(c[0].item()) for c in allc]
+    nby = [int(c[1].item()) for c in allc]
     if rank == 0:
-        out = [payload]
-        bufs = {r: torch.empty(max(sizes[r], 1), dtype=torch.uint8, device=device) for r in range(1, world)}
-        ops = [dist.P2POp(dist.irecv, bufs[r], r, group=group) for r in range(1, world) if sizes[r]]
+        body = torch.empty(sum(nby), dtype=torch.uint8, device=device)
+        fsz = torch.empty(sum(nfr), dtype=torch.int32, device=device)
+        body[: nby[0]].copy_(frames)
+        fsz[: nfr[0]].copy_(sizes)
+        ops, ob, of = [], nby[0], nfr[0]
+        for r in range(1, world):
+            if nfr[r]:
+                ops.append(dist.P2POp(dist.irecv, fsz[of:of + nfr[r]], r, group=group))
+            if nby[r]:
+                ops.append(dist.P2POp(dist.irecv, body[ob:ob + nby[r]], r, group=group))
+            ob += nby[r]
+            of += nfr[r]
         for req in (dist.batch_isend_irecv(ops) if ops else []):
             req.wait()
-        for r in range(1, world):
-            out.append(bytes(bufs[r][: sizes[r]].cpu().numpy().tobytes()) if sizes[r] else b"")
-        return out
-    if sizes[rank]:
-        import numpy as np
-
-        t = torch.from_numpy(np.frombuffer(payload, dtype=np.uint8).copy()).to(device)
-        for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, 0, group=group)]):
-            req.wait()
+        return body, fsz
+    ops = []
+    if nfr[rank]:
+        ops.append(dist.P2POp(dist.isend, sizes.contiguous(), 0, group=group))
+    if nby[rank]:
+        ops.append(dist.P2POp(dist.isend, frames.contiguous(), 0, group=group))
+    for req in (dist.batch_isend_irecv(ops) if ops else []):
+        req.wait()
     return None
+
+
+def _encode_shard(encoder, pcm: bytes, per: int, s0: int, s1: int, f0: int, device):
+    """This rank's frames as tensors on `device`: on a GPU the bitstream never leaves HBM."""
+    import numpy as np
+    import torch
+
+    if s1 <= s0:
+        return torch.empty(0, dtype=torch.uint8, device=device), torch.empty(0, dtype=torch.int32, device=device)
+    if hasattr(encoder, "encode_frames_device"):
+        src = torch.from_numpy(np.frombuffer(pcm, dtype=np.uint8, count=(s1 - s0) * per, offset=s0 * per).copy())
+        d_pcm = src.to(torch.device("cuda", torch.cuda.current_device()))
+        frames, sizes = encoder.encode_frames_device(d_pcm.data_ptr(), s1 - s0, first_frame=f0)
+        return frames.to(device), sizes.to(device)  # no copy when `device` is this GPU (RCCL)
+    frames, sizes = encoder.encode_frames(pcm[s0 * per:s1 * per], first_frame=f0)
+    return (torch.from_numpy(np.frombuffer(frames, dtype=np.uint8).copy()).to(device),
+            torch.tensor(sizes, dtype=torch.int32, device=device))
 
 
 def encode_sharded(encoder, pcm: bytes, dist=None, group=None, device="cpu", md5: str = "host") -> Optional[bytes]:
     """Encode one stream (interleaved LE PCM, identical on every rank) across the ranks of
     `group`; returns the whole .flac file on rank 0 and None elsewhere.
 
-    `encoder` provides channels, bits, sample_rate, bytes_per_sample, block_size and
-    encode_frames(pcm, first_frame) -> (bytes, sizes) (flacgpu.Encoder on a GPU).
+    `encoder` provides channels, bits, sample_rate, bytes_per_sample, block_size and either
+    encode_frames_device(d_pcm, n, first_frame) -> (uint8 tensor, int32 tensor) on a GPU
+    (flacgpu.Encoder; frames stay in HBM) or encode_frames(pcm, first_frame) -> (bytes,
+    sizes).  `device` is where the gather's tensors live ("cuda:k" for RCCL, "cpu" for gloo).
     """
+    import ctypes
+
     world = dist.get_world_size(group) if dist else 1
     rank = dist.get_rank(group) if dist else 0
     per = encoder.channels * encoder.bytes_per_sample
@@ -76,28 +119,17 @@ def encode_sharded(encoder, pcm: bytes, dist=None, group=None, device="cpu", md5
     if rank == 0 and md5 == "host":
         th = threading.Thread(target=lambda: digest.setdefault("md5", hashlib.md5(pcm).digest()))
         th.start()
-    frames, sizes = encoder.encode_frames(pcm[s0 * per:s1 * per], first_frame=f0) if s1 > s0 else (b"", [])
+    frames, sizes = _encode_shard(encoder, pcm, per, s0, s1, f0, device)
     if rank == 0 and md5 == "gpu":
         digest["md5"] = encoder.md5(pcm)
-
-    # payload: u32 frame count, u32 sizes..., frame bytes
-    import struct
-
-    payload = struct.pack(f"<I{len(sizes)}I", len(sizes), *sizes) + frames
-    parts = _gather_bytes(dist, group, payload, device, rank, world) if dist else [payload]
+    got = gather_frames(dist, group, frames, sizes, rank, world) if dist else (frames, sizes)
     if rank != 0:
         return None
+    body, fsz = got
     if th:
         th.join()
-    all_sizes, body = [], []
-    for p in parts:
-        k = struct.unpack_from("<I", p)[0]
-        all_sizes += list(struct.unpack_from(f"<{k}I", p, 4))
-        body.append(p[4 + 4 * k:])
-    si = flacgpu.StreamInfo.new(encoder.sample_rate, encoder.channels, encoder.bits, n)
-    for sz in all_sizes:
+    si = flacgpu.StreamInfo.new(encoder.sample_rate, encoder.channels, encoder.bits, n, encoder.block_size)
+    for sz in fsz.cpu().tolist():
         si.update_frame_size(sz)
-    import ctypes
-
     ctypes.memmove(si.md5, digest["md5"], 16)
-    return flacgpu.header_bytes(si, False) + flacgpu.vorbis_comment_bytes(True) + b"".join(body)
+    return flacgpu.header_bytes(si, False) + flacgpu.vorbis_comment_bytes(True) + body.cpu().numpy().tobytes()
