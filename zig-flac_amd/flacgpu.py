@@ -170,6 +170,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise FileNotFoundError(f"{path} not built: run `make -C zig-flac_amd` (or __graft_entry__.build())")
+    # PyTorch-ROCm bundles its own HIP/HSA runtime under the same SONAME (libamdhip64.so.7).
+    # Loaded first, it is the one libflacgpu.so binds to, so device pointers and streams of
+    # torch tensors and of this library share one runtime.  Loaded after /opt/rocm's copy,
+    # it would start a second HSA runtime on the same device, which fails to initialise
+    # ("No HIP GPUs are available").  So torch, when present, is imported before the library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     P, U32, U64, I32, SZ = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
     sig = {
