@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU parity tests (selection), then one bench line per BASELINE config.  Usage: tools/gpu_cfgs.sh <tag> "<configs>" [pytest selection]
+set -o pipefail
+TAG=$1; CFGS=$2; shift 2
+SEL=${@:-tests}
+mkdir -p gpurun_out
+bash tools/gpu_tests.sh $TAG $SEL || exit 1
+for C in $CFGS; do
+  timeout -k 10 200 python bench.py --config $C --steps 5 --warmup 2 --no-cpu --no-curve --no-e2e --verify-streams 8 > gpurun_out/cfg_${TAG}_$C.json 2> gpurun_out/cfg_${TAG}_$C.err || { echo "FAIL $C"; tail -3 gpurun_out/cfg_${TAG}_$C.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['output_ok'], d['kernel_ms_per_step'])" gpurun_out/cfg_${TAG}_$C.json $C
+done

@@ -10,13 +10,15 @@ NAMES = ["DMA issue+job load", "sample load", "waste+eq", "bestOrder", "rice pas
 PNAMES = ["top barrier", "offsets+bar", "zero img+bars", "residuals", "pack codes+bar", "CRC+bars", "store+bar",
           "ticket+desc loads", "vmcnt(0) wait", "DMA issue+sample load", "lane_bits/bits loads+scan"]
 S, F = 1024, 32
-enc = flacgpu.Encoder(2, 16, 44100, max_frames=S * F)
+CH, BITS, RATE = int(os.environ.get("CH", "2")), int(os.environ.get("BITS", "16")), int(os.environ.get("RATE", "44100"))
+FB = CH * BITS // 8
+enc = flacgpu.Encoder(CH, BITS, RATE, max_frames=S * F)
 L = enc.lib
 L.flacgpu_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-pool = synth.synth_samples(4096 * 256, 2, 16, 44100)
-pcm = np.frombuffer(synth.to_pcm_bytes(pool, 16), dtype=np.uint8)
-buf = np.concatenate([pcm[(s % 8) * 4096 * 4 * 16:][: F * 4096 * 4] for s in range(S)])
-plan = enc.plan([s * F * 4096 * 4 for s in range(S)], [F * 4096] * S)
+pool = synth.synth_samples(4096 * 256, CH, BITS, RATE)
+pcm = np.frombuffer(synth.to_pcm_bytes(pool, BITS), dtype=np.uint8)
+buf = np.concatenate([pcm[(s % 8) * 4096 * FB * 16:][: F * 4096 * FB] for s in range(S)])
+plan = enc.plan([s * F * 4096 * FB for s in range(S)], [F * 4096] * S)
 d_pcm = torch.from_numpy(buf).cuda()
 d_out = torch.empty(int(plan.out_bound), dtype=torch.uint8, device="cuda")
 d_fb = torch.empty(plan.n_frames, dtype=torch.int32, device="cuda")

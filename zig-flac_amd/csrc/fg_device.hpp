@@ -561,6 +561,17 @@ __device__ __forceinline__ void load_candidate(const uint32_t *stg, uint32_t cst
             else put([](int32_t L, int32_t R) { return L - R; });
             __builtin_amdgcn_sched_barrier(0);
         }
+    } else if constexpr (B == 3) {
+        // 24-bit: the two dwords around the sample (a ds_read2_b32) and v_alignbyte, instead of
+        // three byte loads per sample
+        const uint32_t CB = C * 3u;
+        auto ld24 = [&](uint32_t off) -> int64_t {
+            const uint32_t w = off >> 2, o = off & 3u;
+            const uint32_t v = __builtin_amdgcn_alignbyte(lw[w + 1u], lw[w], o);
+            return (int32_t)(v << 8) >> 8;
+        };
+        fill([&](int j, uint32_t c) -> int64_t { return ld24((uint32_t)j * CB + 3u * c); },
+             [&](int j) -> int64_t { return ld24((uint32_t)j * CB + 3u); });
     } else {
         const uint8_t *base = (const uint8_t *)lw;
         const uint32_t CB = C * B;
@@ -924,8 +935,16 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.stage1 : LY.stage0));
 
         // ---- 1. the frame's interleaved PCM in LDS (64 padded chunks of 64 samples)
-        if (dbuf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+        if (dbuf) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if constexpr (FULL) {
+            // one buffer (the frame is too large for two): every wave issues all its LDS-DMA
+            // loads at once and waits once -- not one load-store round trip per dword
+            stage_dma(a.pcm, job.pcm_off, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+        }
         STAMP(9);
         __syncthreads();
         STAMP(10);
@@ -1752,8 +1771,16 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
 
         // ---- 1. PCM -> LDS (already in flight with double buffering), candidate samples -> VGPRs
         STAMP(7);
-        if (dbuf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+        if (dbuf) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if constexpr (FULL) {
+            // one buffer (the frame is too large for two): every wave issues all its LDS-DMA
+            // loads at once and waits once -- not one load-store round trip per dword
+            stage_dma(a.pcm, job.pcm_off, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+        }
         STAMP(8);
         __syncthreads();
         STAMP(0);

@@ -199,11 +199,19 @@ __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16
 // shares on the same CU, 4x less busy.
 typedef uint32_t md5_v4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FG_MD5_AHEAD
-#define FG_MD5_AHEAD 2
+#define FG_MD5_AHEAD 1
+#endif
+// waves per SIMD the MD5 kernel is compiled for: at 7 it fits 72 VGPRs (one message block in flight ahead), so its waves take
+// little of the register file the encode kernels running beside it occupy
+#ifndef FG_MD5_WPE
+#define FG_MD5_WPE 7
 #endif
 constexpr int kMd5Ahead = FG_MD5_AHEAD;
 
 __device__ __forceinline__ void md5_load_block(const uint8_t *p, uint32_t (&m)[16]) {
+#if defined(FG_MD5_DIAG) && FG_MD5_DIAG == 1
+    p = (const uint8_t *)((uintptr_t)p & ~(uintptr_t)0xFFFF);  // diagnostics: a cache-resident block
+#endif
     const md5_v4 *q = (const md5_v4 *)p;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -215,7 +223,7 @@ __device__ __forceinline__ void md5_load_block(const uint8_t *p, uint32_t (&m)[1
     }
 }
 
-__global__ void __launch_bounds__(64) k_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FG_MD5_WPE, 8))) k_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens,
                                                     const uint8_t *final_flags, uint32_t n_streams, Md5State *states,
                                                     uint8_t *digests) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -258,25 +266,36 @@ __global__ void __launch_bounds__(64) k_md5_streams(const uint8_t *base, const u
     for (int k = 0; k < kMd5Ahead; k++)
         if (b + k < full) md5_compress(st, m[k]);
     if (fin) {
-        // tail + padding (one or two blocks), assembled straight into message words
+        // tail + padding (one or two blocks): the rem < 64 tail bytes as dwords (the dword holding
+        // the end assembled from bytes: nothing past the segment is read), then 0x80 and the
+        // bit length
         const uint32_t rem = (uint32_t)(len & 63);
         const uint8_t *tp = p + full * 64;
-        const uint32_t nb = rem < 56 ? 1u : 2u;
-        const uint64_t bits = (done + len) * 8;
-        for (uint32_t bb = 0; bb < nb; bb++) {
-            uint32_t mt[16];
+        const uint32_t *tp32 = (const uint32_t *)tp;
+        uint32_t mt[16];
+        const uint32_t wr = rem >> 2, br = rem & 3u;
 #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const uint32_t idx = bb * 64u + 4u * i + q;
-                    uint32_t by = idx < rem ? tp[idx] : (idx == rem ? 0x80u : 0u);
-                    if (bb == nb - 1 && 4 * i + q >= 56) by = (uint32_t)(bits >> (8 * (4 * i + q - 56))) & 255u;
-                    v |= by << (8 * q);
-                }
-                mt[i] = v;
+        for (int i = 0; i < 16; i++) {
+            uint32_t v = 0;
+            if ((uint32_t)i < wr) {
+                v = tp32[i];
+            } else if ((uint32_t)i == wr) {
+                for (uint32_t q = 0; q < br; q++) v |= (uint32_t)tp[4u * i + q] << (8u * q);
+                v |= 0x80u << (8u * br);
             }
+            mt[i] = v;
+        }
+        const uint64_t bits = (done + len) * 8;
+        if (rem < 56) {
+            mt[14] = (uint32_t)bits;
+            mt[15] = (uint32_t)(bits >> 32);
+            md5_compress(st, mt);
+        } else {
+            md5_compress(st, mt);
+#pragma unroll
+            for (int i = 0; i < 14; i++) mt[i] = 0;
+            mt[14] = (uint32_t)bits;
+            mt[15] = (uint32_t)(bits >> 32);
             md5_compress(st, mt);
         }
         if (digests)
