@@ -627,6 +627,62 @@ __device__ __forceinline__ bool load_lpc_samples(const uint32_t *stg, uint32_t c
     }
 }
 
+// 32-bit input (CLS 32): samples held compactly as their low 32 bits plus one mask bit per
+// sample (bit j of hb = bit 32 of sample j, i.e. the sign of the 33-bit side of
+// encoder.zig:330-339; for every other candidate the sign of a value that fits i32).  Half
+// the registers of an i64 array: the 32-bit kernels held 128 VGPRs of samples and spilled.
+// The i64 value is rebuilt only where exact 64-bit arithmetic is needed (bestOrder's wide
+// mode, fixed.zig:85-167); residuals truncated to i32 (fixed.zig:69-74) follow from the low
+// words alone, since a sample and its low word agree mod 2^32.
+__device__ __forceinline__ int64_t wide_value(int32_t lo, uint64_t hb, int j) {
+    const uint32_t hi = ((hb >> j) & 1ull) ? 0xFFFFFFFFu : 0u;
+    return (int64_t)(((uint64_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+template <int B, bool FULL, int NC>
+__device__ __forceinline__ void load_candidate32(const uint32_t *stg, uint32_t cst, uint32_t l, uint32_t n, bool stereo,
+                                                 uint32_t cand, uint32_t C, int32_t (&s)[64], uint64_t &hb) {
+    const uint32_t *lw = stg + l * cst;
+    const uint32_t kind = stereo ? cand : 0u;  // 0 plain channel, 1 R, 2 mid, 3 side
+    const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand;
+    hb = 0;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) {
+            const int j = 16 * g + jj;
+            int64_t L, Rr;
+            if constexpr (NC == 2) {
+                const uint2 v = ((const uint2 *)lw)[j];
+                L = (int32_t)(chan ? v.y : v.x);
+                Rr = (int32_t)v.y;
+                if (kind >= 2) L = (int32_t)v.x;
+            } else {
+                const uint8_t *base = (const uint8_t *)lw;
+                L = ld_sample<4>(base + j * C * 4u + chan * 4u);
+                Rr = 0;
+            }
+            int64_t v = kind <= 1 ? L : (kind == 2 ? (L + Rr) >> 1 : L - Rr);
+            if (!FULL && l * 64u + j >= n) v = 0;
+            s[j] = (int32_t)v;
+            hb |= (uint64_t)((v >> 32) & 1) << j;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+// the waste shift (encoder.zig:556-570) of the compact form: v >> w for 0 < w < bd (<= 33);
+// the result fits i32, so its mask bits become the signs
+__device__ __forceinline__ void shift32(int32_t (&s)[64], uint64_t &hb, uint32_t w) {
+    uint64_t nb = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const uint32_t hi = ((hb >> j) & 1ull) ? 0xFFFFFFFFu : 0u;
+        const uint32_t v = w < 32u ? __builtin_amdgcn_alignbit(hi, (uint32_t)s[j], w) : hi;
+        s[j] = (int32_t)v;
+        nb |= (uint64_t)(v >> 31) << j;
+    }
+    hb = nb;
+}
+
 // Fixed-predictor residual of order K from sample x and history q1..q4
 // (fixed.zig:12-18 COEFF_SCALAR stencil): wrapping i32 (narrow, fixed.zig:63-68)
 // or exact i64 truncated to i32 (wide, fixed.zig:69-74).
@@ -958,8 +1014,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         STAMP(0);
 
         // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
-        ST s[64];
-        load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, s);
+        // (32-bit input: low words + the bit-32 mask, see load_candidate32)
+        using SS = typename std::conditional<CLS == 32, int32_t, ST>::type;
+        SS s[64];
+        uint64_t hb = 0;
+        if constexpr (CLS == 32) load_candidate32<B, FULL, NC>(stg, cst, l, n, stereo, cand, C, s, hb);
+        else load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, s);
         STAMP(1);
 
         // ---- 3. wasted bits (encoder.zig:556-570)
@@ -976,22 +1036,37 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 for (int j = 0; j < 64; j++) o32 |= (uint32_t)s[j];
                 o = wave_or32(o32);
             } else {
-                uint64_t o64 = 0;
+                uint32_t o32 = 0;
 #pragma unroll
-                for (int j = 0; j < 64; j++) o64 |= (uint64_t)s[j];
-                o = wave_or64(o64);
+                for (int j = 0; j < 64; j++) o32 |= (uint32_t)s[j];
+                o = wave_or64((uint64_t)o32 | (hb ? 0xFFFFFFFF00000000ull : 0ull));
             }
             const uint32_t w = (o == 0) ? bd : (uint32_t)__builtin_ctzll(o);
             if (w != 0 && w != bd) {
+                if constexpr (CLS == 32) {
+                    shift32(s, hb, w);
+                } else {
 #pragma unroll
-                for (int j = 0; j < 64; j++) s[j] >>= w;
+                    for (int j = 0; j < 64; j++) s[j] >>= w;
+                }
             }
             R.waste = w;
         }
         const uint32_t bps = bd - R.waste;
 
         // history: the 4 samples before this lane's chunk (lane 0 gets zeros; its i<k terms are masked)
-        const ST h1 = shr1(s[63]), h2 = shr1(s[62]), h3 = shr1(s[61]), h4 = shr1(s[60]);
+        // (32-bit input: hl* the low words for the truncated residuals, h* the exact values)
+        const SS hl1 = shr1(s[63]), hl2 = shr1(s[62]), hl3 = shr1(s[61]), hl4 = shr1(s[60]);
+        ST h1, h2, h3, h4;
+        if constexpr (CLS == 32) {
+            const uint64_t hbp = (uint64_t)shr1_32((uint32_t)(hb >> 32)) << 32;  // the previous lane's bits 32..63
+            h1 = wide_value(hl1, hbp, 63);
+            h2 = wide_value(hl2, hbp, 62);
+            h3 = wide_value(hl3, hbp, 61);
+            h4 = wide_value(hl4, hbp, 60);
+        } else {
+            h1 = hl1; h2 = hl2; h3 = hl3; h4 = hl4;
+        }
 
         // ---- 4. CONSTANT / VERBATIM defaults (encoder.zig:493-514)
         bool try_fixed = false;
@@ -1001,7 +1076,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         } else {
             ST x0;
             if constexpr (CLS != 32) x0 = (ST)rdl((uint32_t)s[0], 0);
-            else x0 = (ST)rdl64((uint64_t)s[0], 0);
+            else x0 = wide_value((int32_t)rdl((uint32_t)s[0], 0), (uint64_t)(rdl((uint32_t)hb, 0) & 1u), 0);
             bool eq = true;
             if constexpr (CLS != 32) {
                 // all equal to x0 <=> max == min == x0: v_max3/v_min3 over the samples instead of a
@@ -1016,7 +1091,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 eq = (mx == (int32_t)x0) && (mn == (int32_t)x0);
             } else {
 #pragma unroll
-                for (int j = 0; j < 64; j++) eq &= (s[j] == x0) || (!FULL && l * 64u + j >= n);
+                for (int j = 0; j < 64; j++) eq &= (wide_value(s[j], hb, j) == x0) || (!FULL && l * 64u + j >= n);
             }
             if (__all(eq)) {
                 R.type = 0;
@@ -1146,7 +1221,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 for (int j = 0; j < 64; j++) {
                     const bool valid = FULL || (l * 64u + j < n);
                     const bool z = (l == 0);
-                    const int64_t e0 = s[j], e1 = e0 - p0, e2 = e1 - p1, e3 = e2 - p2, e4 = e3 - p3;
+                    const int64_t e0 = wide_value(s[j], hb, j), e1 = e0 - p0, e2 = e1 - p1, e3 = e2 - p2,
+                                  e4 = e3 - p3;
                     const uint64_t a0 = (uint64_t)(e0 < 0 ? -e0 : e0), a1 = (uint64_t)(e1 < 0 ? -e1 : e1),
                                    a2 = (uint64_t)(e2 < 0 ? -e2 : e2), a3 = (uint64_t)(e3 < 0 ? -e3 : e3),
                                    a4 = (uint64_t)(e4 < 0 ? -e4 : e4);
@@ -1158,6 +1234,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     A3 += v3 ? a3 : 0; O3 |= v3 ? a3 : 0;
                     A4 += v4 ? a4 : 0; O4 |= v4 ? a4 : 0;
                     p0 = e0; p1 = e1; p2 = e2; p3 = e3;
+                    // keep the ten accumulations serial: reassociated into trees they would hold all
+                    // 64 terms of each live at once (hundreds of VGPRs, spilled)
+                    asm volatile("" : "+v"(A0), "+v"(A1), "+v"(A2), "+v"(A3), "+v"(A4));
+                    asm volatile("" : "+v"(O0), "+v"(O1), "+v"(O2), "+v"(O3), "+v"(O4));
                 }
                 T[0] = wave_or64(O0) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A0);
                 T[1] = wave_or64(O1) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A1);
@@ -1214,6 +1294,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             if constexpr (FULL) {
                 S8[j >> 4] += warm ? 0u : av;
                 O8[j >> 4] |= warm ? 0u : zz;
+                if constexpr (CLS == 32) asm volatile("" : "+v"(S8[j >> 4]));  // serial 64-bit sums
             } else {
                 const uint32_t i = l * 64u + j;
                 if (!warm && i < n) {
@@ -1380,11 +1461,11 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
 #pragma unroll
                 for (int g = 0; g < 4; g++)
                     S8[g] = k == 0 ? tg[0][g] : k == 1 ? tg[1][g] : k == 2 ? tg[2][g] : k == 3 ? tg[3][g] : tg[4][g];
-                auto acc = [&](int j, bool warm, ST r) { O8[j >> 4] |= warm ? 0u : zigzag32((int32_t)r); };
-                FG_DISPATCH_K(k, (residuals_k<K, ST>(s, h1, h2, h3, h4, l, acc)))
+                auto acc = [&](int j, bool warm, SS r) { O8[j >> 4] |= warm ? 0u : zigzag32((int32_t)r); };
+                FG_DISPATCH_K(k, (residuals_k<K, SS>(s, hl1, hl2, hl3, hl4, l, acc)))
             } else {
-                auto acc = [&](int j, bool warm, ST r) { part_acc(S8, O8, ps, j, warm, (int32_t)r); };
-                FG_DISPATCH_K(k, (residuals_k<K, ST>(s, h1, h2, h3, h4, l, acc)))
+                auto acc = [&](int j, bool warm, SS r) { part_acc(S8, O8, ps, j, warm, (int32_t)r); };
+                FG_DISPATCH_K(k, (residuals_k<K, SS>(s, hl1, hl2, hl3, hl4, l, acc)))
             }
             STAMP(4);
 
@@ -1549,14 +1630,20 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                                                         [&](int j, bool warm, int64_t e) { f(j, warm, (ST)(int32_t)e); });
                         }
                     } else {
-                        ST t[64];
-                        load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, t);
-                        if (w != 0) {
+                        SS t[64];
+                        if constexpr (CLS == 32) {
+                            uint64_t hbt;
+                            load_candidate32<B, FULL, NC>(stg, cst, l, n, stereo, cand, C, t, hbt);
+                            if (w != 0) shift32(t, hbt, w);
+                        } else {
+                            load_candidate<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, t);
+                            if (w != 0) {
 #pragma unroll
-                            for (int j = 0; j < 64; j++) t[j] >>= w;
+                                for (int j = 0; j < 64; j++) t[j] >>= w;
+                            }
                         }
-                        const ST g1 = shr1(t[63]), g2 = shr1(t[62]), g3 = shr1(t[61]), g4 = shr1(t[60]);
-                        FG_DISPATCH_K(k, (residuals_k<K, ST>(t, g1, g2, g3, g4, l, f)))
+                        const SS g1 = shr1(t[63]), g2 = shr1(t[62]), g3 = shr1(t[61]), g4 = shr1(t[60]);
+                        FG_DISPATCH_K(k, (residuals_k<K, SS>(t, g1, g2, g3, g4, l, f)))
                     }
                 };
                 if constexpr (FULL) {
