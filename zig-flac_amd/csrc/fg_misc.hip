@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FG_MD5_
     // The chain is latency-bound and these few waves share SIMDs with the encode kernels.  At
     // issue priority 3 they win every arbitration and the encode waves beside them lose issue
     // slots; at the default 0 the encode runs ~5-10 % faster with 16384 streams while each MD5
-    // chain slows only slightly (profiles/r2c_*).
+    // chain slows only slightly (tools/ab_md5.sh A/B).
 #ifndef FG_MD5_PRIO
 #define FG_MD5_PRIO 0
 #endif
