@@ -12,7 +12,8 @@ PNAMES = ["top barrier", "offsets+bar", "zero img+bars", "residuals", "pack code
 S, F = 1024, 32
 CH, BITS, RATE = int(os.environ.get("CH", "2")), int(os.environ.get("BITS", "16")), int(os.environ.get("RATE", "44100"))
 FB = CH * BITS // 8
-enc = flacgpu.Encoder(CH, BITS, RATE, max_frames=S * F)
+LPC = int(os.environ.get("LPC", "0"))
+enc = flacgpu.Encoder(CH, BITS, RATE, max_frames=S * F, lpc_order=LPC)
 L = enc.lib
 L.flacgpu_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 pool = synth.synth_samples(4096 * 256, CH, BITS, RATE)
@@ -36,9 +37,11 @@ for _ in range(5):
 torch.cuda.synchronize()
 print("encode ms/launch", enc.kernel_time(0))
 L.flacgpu_debug_stamps(enc.ctx, out, 0)
+WA = 4 if CH == 2 else CH                        # analysis waves per frame (stereo: L, R, M, S)
+WP = 8 if (CH == 2 and BITS == 16) else CH       # pack waves per frame (k_pack4: 4 per written subframe)
 for base, names, label in [(0, NAMES, "analysis"), (16, PNAMES, "pack")]:
     tot = sum(out[base:base + len(names)])
     print(f"-- {label}")
     for i, n in enumerate(names):
         v = out[base + i]
-        print(f"{i:2d} {n:20s} {v / max(tot,1) * 100:6.2f}%  {v / (5 * S * F * (4 if base == 0 else 2)):10.1f} clk/wave-frame")
+        print(f"{i:2d} {n:20s} {v / max(tot,1) * 100:6.2f}%  {v / (5 * S * F * (WA if base == 0 else WP)):10.1f} clk/wave-frame")

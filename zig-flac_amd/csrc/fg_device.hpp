@@ -21,6 +21,10 @@
 
 namespace fg {
 
+// compile-time value tag for uniform dispatch (one branch around a loop, not one per element)
+template <uint32_t V>
+using ic = std::integral_constant<uint32_t, V>;
+
 // ------------------------------------------------------------------------
 // wave64 helpers
 // ------------------------------------------------------------------------

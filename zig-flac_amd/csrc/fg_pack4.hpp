@@ -40,6 +40,13 @@ __device__ __forceinline__ void stage_dma_rot(const uint8_t *pcm, uint64_t off, 
     }
 }
 
+// OR two words into LDS at byte address addr (4-aligned) and addr + 4.  Inline asm: the
+// address is an absolute LDS address, so no base add per code; the ORs are ordered before
+// any read of the image by the lgkmcnt(0) of the next bar_lds().
+__device__ __forceinline__ void lds_or2(uint32_t addr, uint32_t hi, uint32_t lo) {
+    asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(addr), "v"(hi), "v"(lo) : "memory");
+}
+
 // dword offset of 4-sample group g of 16-sample chunk j in the rotated layout
 __device__ __forceinline__ uint32_t rot_off(uint32_t j, uint32_t g) { return 16u * j + 4u * ((g + (j >> 2)) & 3u); }
 
@@ -67,6 +74,10 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
     if (jidx < a.n_jobs) job = a.jobs[jidx];
     if (nxt < a.n_jobs) jn = a.jobs[nxt];
     if (jidx < a.n_jobs) stage_dma_rot(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), wave, NW, l0);
+#ifdef FG_STAMPS
+    uint64_t ph_[16] = {};
+    uint64_t tprev_ = __builtin_amdgcn_s_memtime();
+#endif
     while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);
         if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
@@ -81,9 +92,9 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         const uint64_t D = a.offsets[job.slot];
         const uint32_t Lb = (total_bits + 7u) >> 3;
         const uint32_t W4 = Lb >> 2;
-        const uint32_t H = ((W4 + 2u * NT - 1u) / (2u * NT)) | 1u;
+        const uint32_t H = max((W4 + 2u * NT - 1u) / (2u * NT), 1u);  // words per thread / 2
         const uint32_t hq = min(H, a.crc_hmax4) - 1u;
-        const uint32_t crc_jw = a.crc_join[hq], crc_pw = a.crc_pow4[hq * NT + tid];
+        const uint32_t crc_pw = a.crc_pow4[hq * NT + tid];
         const bool skip = fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap;  // uniform
         const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
                        method = sd->method, cand = sd->cand;
@@ -94,8 +105,11 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         if (sfi) sub_start += sd0->bits;
 
         // ---- 1. PCM (DMA'd during the previous frame) -> this lane's samples and their history
+        STAMP(7);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(8);
         __syncthreads();
+        STAMP(0);
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         if (nxt < a.n_jobs) stage_dma_rot(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), wave, NW, l);
         FrameJob jnn{};
@@ -117,20 +131,33 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
                 raw[4 + 4 * g] = v.x; raw[5 + 4 * g] = v.y; raw[6 + 4 * g] = v.z; raw[7 + 4 * g] = v.w;
             }
         }
-        // candidate samples (stereo: 0 L, 1 R, 2 mid, 3 side; otherwise channel `cand`)
+        STAMP(9);
+        // candidate samples (stereo: 0 L, 1 R, 2 mid, 3 side; otherwise channel `cand`).  The
+        // candidate and the predictor order are uniform: one dispatch each around the whole lane
+        // loop, not a branch ladder per sample.
         const uint32_t kind = stereo ? cand : (cand ? 1u : 0u);
         int32_t x[20];
+        auto unpack = [&](auto KD) {
+            constexpr uint32_t KND = decltype(KD)::value;
 #pragma unroll
-        for (int i = 0; i < 20; i++) {
-            const int32_t L = (int32_t)(raw[i] << 16) >> 16, R = (int32_t)raw[i] >> 16;
-            x[i] = kind == 0 ? L : kind == 1 ? R : kind == 2 ? (L + R) >> 1 : L - R;
-        }
+            for (int i = 0; i < 20; i++) {
+                const int32_t L = (int32_t)(raw[i] << 16) >> 16, R = (int32_t)raw[i] >> 16;
+                x[i] = KND == 0 ? L : KND == 1 ? R : KND == 2 ? (L + R) >> 1 : L - R;
+            }
+        };
+        if (kind == 0) unpack(ic<0>{});
+        else if (kind == 1) unpack(ic<1>{});
+        else if (kind == 2) unpack(ic<2>{});
+        else unpack(ic<3>{});
         // lane offsets: quarter base = the analysis kernel's segment lengths before it
         const uint32_t lbs = wave_incl_scan32(lb);
         const uint32_t qbase = qw ? rdl(lbs, (int)(16u * qw - 1u)) : 0u;
+        STAMP(10);
         bar_lds();  // staging dead: zero the image
+        STAMP(1);
         const uint32_t Wz = (fbytes + 3u) / 4u + 2u;
         for (uint32_t i = tid; i < Wz; i += NT) img[i] = 0;
+        STAMP(2);
 
         // ---- 2. waste shift and residuals (fixed.zig:30-81), lengths of this lane's codes
         const uint32_t bps = bd - w;
@@ -143,23 +170,34 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         const bool esc = (p & 0x80u) != 0;
         const uint32_t wb = p & 0x7Fu, pr = esc ? 0u : p;
         uint32_t r[16];
-        if (type == 2) {
+        auto resid = [&](auto KO) {
+            constexpr uint32_t K = decltype(KO)::value;
 #pragma unroll
             for (int i = 0; i < 16; i++) {
                 const uint32_t u0 = (uint32_t)x[4 + i], u1 = (uint32_t)x[3 + i], u2 = (uint32_t)x[2 + i],
                                u3 = (uint32_t)x[1 + i], u4 = (uint32_t)x[i];
-                uint32_t e;
-                if (k == 0) e = u0;
-                else if (k == 1) e = u0 - u1;
-                else if (k == 2) e = (u0 + u2) - 2u * u1;
-                else if (k == 3) e = (u0 - u3) + 3u * (u2 - u1);
-                else e = (u0 + u4) - 4u * (u1 + u3) + 6u * u2;
-                r[i] = e;
+                if constexpr (K == 0) r[i] = u0;
+                else if constexpr (K == 1) r[i] = u0 - u1;
+                else if constexpr (K == 2) r[i] = (u0 + u2) - 2u * u1;
+                else if constexpr (K == 3) r[i] = (u0 - u3) + 3u * (u2 - u1);
+                else r[i] = (u0 + u4) - 4u * (u1 + u3) + 6u * u2;
             }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; i++) r[i] = (uint32_t)x[4 + i];
-        }
+        };
+        if (type != 2 || k == 0) resid(ic<0>{});
+        else if (k == 1) resid(ic<1>{});
+        else if (k == 2) resid(ic<2>{});
+        else if (k == 3) resid(ic<3>{});
+        else resid(ic<4>{});
+        // per-lane code shape (a lane's 16 samples share one partition, >= 16 samples):
+        // rice = q zeros, then (1 << p) | low p bits in cl = p + 1 bits; escape = the raw
+        // wb-bit two's complement value, no unary part.  Warm-up samples (the subframe's first
+        // k, lane 0 of quarter 0) are written by the header writer and code as nothing here.
+        const uint32_t cl = esc ? wb : pr + 1u;
+        const uint32_t cmask = esc ? ((1u << wb) - 1u) : ((1u << pr) - 1u);  // wb <= 31
+        const uint32_t cbit = esc ? 0u : (1u << pr);
+        const uint32_t qmask = esc ? 0u : ~0u;
+        const uint32_t nwarm = (first && type == 2) ? k : 0u;
+        auto warm_at = [&](int i) -> bool { return i < 4 && (uint32_t)i < nwarm; };
         // header bits (lane 0 of the subframe) and partition header bits (a lane opening a partition)
         uint32_t len = 0;
         if (first) {
@@ -172,15 +210,17 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         if (type == 1) {
             len += 16u * bps;
         } else if (type == 2) {
+            uint32_t qs = 0;
 #pragma unroll
             for (int i = 0; i < 16; i++) {
-                const bool warm = first && (uint32_t)i < k;
-                const uint32_t zz = zigzag32((int32_t)r[i]);
-                len = add_chain(len, warm ? 0u : (esc ? wb : (zz >> pr) + 1u + pr));
+                const uint32_t qz = zigzag32((int32_t)r[i]) >> pr;
+                qs = add_chain(qs, warm_at(i) ? 0u : qz);
             }
+            len += (qs & qmask) + (16u - nwarm) * cl;
         }
         const uint32_t lane_off = wave_incl_scan32(len) - len;
         bar_lds();  // image zeroed
+        STAMP(3);
         if (tid < 4) {
             const uint32_t hv = F->hdr[tid];
             if (hv) atomicOr(&img[tid], hv);
@@ -227,37 +267,52 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
                     pos += bps;
                 }
             } else if (type == 2) {
+                // pa: bit address from the LDS base, so a code's word address is (pa >> 5) * 4 and
+                // its 64-bit window shift is (64 - cl) - (pa & 31): v < 2^cl, cl <= 32
+                const uint32_t img_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)img;
+                uint32_t pa = 8u * img_lds + pos;
+                const uint32_t ncl = 64u - cl;
+                auto emit = [&](auto ESC) {
+                    constexpr bool E = decltype(ESC)::value != 0;
 #pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const bool warm = first && (uint32_t)i < k;
-                    const uint32_t zz = zigzag32((int32_t)r[i]);
-                    const uint32_t qz = (esc || warm) ? 0u : (zz >> pr);
-                    const uint64_t v = esc ? ((uint64_t)r[i] & (~0ull >> (64 - (wb ? wb : 1u))))
-                                           : (uint64_t)((1u << pr) | (zz & ((1u << pr) - 1u)));
-                    const uint32_t cl = warm ? 0u : (esc ? wb : pr + 1u);
-                    pos += qz;
-                    put_or2(img, pos, v, cl);
-                    pos += cl;
-                }
+                    for (int i = 0; i < 16; i++) {
+                        const bool warm = warm_at(i);
+                        const uint32_t zz = zigzag32((int32_t)r[i]);
+                        // escape: the residual's two's complement bits
+                        const uint32_t src = E ? (esc ? r[i] : zz) : zz;
+                        uint32_t v = (src & cmask) | cbit;
+                        uint32_t q = E ? ((zz >> pr) & qmask) : (zz >> pr);
+                        uint32_t sh = ncl, adv = cl;
+                        if (i < 4) {
+                            v = warm ? 0u : v;
+                            q = warm ? 0u : q;
+                            sh = warm ? 64u : sh;
+                            adv = warm ? 0u : adv;
+                        }
+                        pa += q;
+                        const uint64_t t = (uint64_t)v << ((sh - (pa & 31u)) & 63u);
+                        lds_or2((pa >> 3) & ~3u, (uint32_t)(t >> 32), (uint32_t)t);
+                        pa += adv;
+                    }
+                };
+                if (__any(esc)) emit(ic<1>{});
+                else emit(ic<0>{});
             }
         }
         bar_lds();
+        STAMP(4);
 
-        // ---- 4. CRC-16 of the frame (front-padded parallel fold, as k_pack)
+        // ---- 4. CRC-16 of the frame: the word stream front-padded with zero words (a no-op for
+        // an init-0 CRC) to NT * 2H words; thread t folds its 2H words in one chain, eight bytes
+        // per step, and shifts the result by z^(64H(NT-1-t)); the workgroup XOR-reduces.
         {
             const int32_t Z = (int32_t)(NT * 2u * H) - (int32_t)W4;
-            uint32_t ca = 0, cb = 0;
-            const int32_t va = (int32_t)(tid * 2u * H) - Z, vb = va + (int32_t)H;
+            uint32_t ca = 0;
+            const int32_t va = (int32_t)(tid * 2u * H) - Z;
             auto word = [&](int32_t rr) -> uint32_t { return rr >= 0 ? img[rr] : 0u; };
-            uint32_t i = 0;
-            for (; i + 1u < H; i += 2u) {
+            for (uint32_t i = 0; i < 2u * H; i += 2u)
                 ca = crc_word2(ca, word(va + (int32_t)i), word(va + (int32_t)i + 1), crct);
-                cb = crc_word2(cb, word(vb + (int32_t)i), word(vb + (int32_t)i + 1), crct);
-            }
-            ca = crc_word(ca, word(va + (int32_t)i), crct);
-            cb = crc_word(cb, word(vb + (int32_t)i), crct);
-            const uint32_t ct = crc_mulmod_t(ca, crc_jw, crct) ^ cb;
-            uint32_t contrib = crc_mulmod_t(ct, crc_pw, crct);
+            uint32_t contrib = crc_mulmod_t(ca, crc_pw, crct);
             contrib = wave_xor32(contrib);
             if (l == 0) misc[wave] = contrib;
         }
@@ -270,30 +325,46 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
             put_bits(img, Lb * 8u, crc, 16);
         }
         bar_lds();
+        STAMP(5);
 
-        // ---- 5. image -> out[D, D + fbytes): big-endian words realigned to the byte offset
+        // ---- 5. image -> out[D, D + fbytes): big-endian words realigned to the byte offset,
+        // 16 bytes per lane and store (edge units of the frame byte-masked)
         {
             const uint64_t E = D + fbytes;
-            const uint64_t q0 = D >> 2, q1 = (E + 3u) >> 2;
             const uint32_t sa = (uint32_t)(D & 3u);
-            uint32_t *o32 = (uint32_t *)a.out;
-            for (uint64_t q = q0 + tid; q < q1; q += NT) {
-                const uint32_t m = (uint32_t)(q - q0);
-                const uint32_t lo = img[m];
-                const uint32_t hi = m ? img[m - 1u] : 0u;
-                const uint32_t v = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(hi, lo, sa) : lo);
-                const uint64_t b0 = 4u * q;
-                if (b0 >= D && b0 + 4u <= E) {
-                    o32[q] = v;
+            const uint64_t qD = D >> 2;
+            for (uint64_t u = (D >> 4) + tid; u < ((E + 15u) >> 4); u += NT) {
+                const int32_t m0 = (int32_t)(4u * u - qD);  // image word of the unit's first word (>= -3)
+                uint32_t v[4];
+                uint32_t prev = m0 >= 1 ? img[m0 - 1] : 0u;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const int32_t m = m0 + c;
+                    const uint32_t lo = m >= 0 ? img[m] : 0u;
+                    v[c] = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(prev, lo, sa) : lo);
+                    prev = lo;
+                }
+                const uint64_t b0 = 16u * u;
+                if (b0 >= D && b0 + 16u <= E) {
+                    *(uint4 *)(a.out + b0) = make_uint4(v[0], v[1], v[2], v[3]);
                 } else {
 #pragma unroll
-                    for (uint32_t b = 0; b < 4; b++)
-                        if (b0 + b >= D && b0 + b < E) a.out[b0 + b] = (uint8_t)(v >> (8 * b));
+                    for (int c = 0; c < 4; c++)
+#pragma unroll
+                        for (uint32_t b = 0; b < 4; b++) {
+                            const uint64_t bb = b0 + 4u * c + b;
+                            if (bb >= D && bb < E) a.out[bb] = (uint8_t)(v[c] >> (8 * b));
+                        }
                 }
             }
         }
         // no barrier here: the image / staging area is next written by the DMA issued after the
         // next frame's top barrier, which already orders this frame's last reads before it
+        STAMP(6);
         jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= 1u;
     }  // persistent frame loop
+#ifdef FG_STAMPS
+    if (l0 == 0 && a.stamps)
+        for (int i = 0; i < 11; i++) atomicAdd(&a.stamps[16 + i], (unsigned long long)ph_[i]);
+#endif
 }
