@@ -254,6 +254,46 @@ __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
     return r & 0xFFFFu;
 }
 
+// OR two words into LDS at byte address addr (4-aligned) and addr + 4.  Inline asm: the
+// address is an absolute LDS address, so no base add per code; the ORs are ordered before
+// any read of the image by the s_waitcnt lgkmcnt(0) of the next barrier.
+__device__ __forceinline__ void lds_or2(uint32_t addr, uint32_t hi, uint32_t lo) {
+    asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(addr), "v"(hi), "v"(lo) : "memory");
+}
+
+// Frame image (big-endian words, bit 0 of the frame = bit 31 of word 0) -> out[D, D + fbytes),
+// realigned to the byte offset D: 16 bytes per thread and store, edge units byte-masked.
+__device__ __forceinline__ void store_frame16(const uint32_t *img, uint8_t *out, uint64_t D, uint32_t fbytes,
+                                              uint32_t tid, uint32_t NT) {
+    const uint64_t E = D + fbytes;
+    const uint32_t sa = (uint32_t)(D & 3u);
+    const uint64_t qD = D >> 2;
+    for (uint64_t u = (D >> 4) + tid; u < ((E + 15u) >> 4); u += NT) {
+        const int32_t m0 = (int32_t)(4u * u - qD);  // image word of the unit's first word (>= -3)
+        uint32_t v[4];
+        uint32_t prev = m0 >= 1 ? img[m0 - 1] : 0u;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const int32_t m = m0 + c;
+            const uint32_t lo = m >= 0 ? img[m] : 0u;
+            v[c] = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(prev, lo, sa) : lo);
+            prev = lo;
+        }
+        const uint64_t b0 = 16u * u;
+        if (b0 >= D && b0 + 16u <= E) {
+            *(uint4 *)(out + b0) = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+#pragma unroll
+                for (uint32_t b = 0; b < 4; b++) {
+                    const uint64_t bb = b0 + 4u * c + b;
+                    if (bb >= D && bb < E) out[bb] = (uint8_t)(v[c] >> (8 * b));
+                }
+        }
+    }
+}
+
 // OR `len` (<= 33) bits of v at bit position pos of the big-endian word image.
 __device__ __forceinline__ void put_bits(uint32_t *img, uint32_t pos, uint64_t v, uint32_t len) {
     if (len == 0) return;
@@ -1913,6 +1953,8 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
             for (int j = 0; j < 64; j++) s[j] >>= w;
         }
         if (type == 2) {
+            // one uniform switch around the lane loop (residuals_k keeps its own history
+            // registers, so writing s[j] from the callback is safe)
             const ST h1 = shr1(s[63]), h2 = shr1(s[62]), h3 = shr1(s[61]), h4 = shr1(s[60]);
             auto none = [](int, bool, ST) {};
             residuals_generic<ST>(s, h1, h2, h3, h4, l, k, none);
@@ -2002,16 +2044,50 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
                     pos += hl;
                 };
                 if constexpr (FULL) {
+                    // per 16-sample group (one partition each: partitions hold >= 16 samples) the
+                    // code shape is lane-constant: rice = q zeros then (1 << p) | low p bits in
+                    // p + 1 bits, escape = the raw wb-bit value; warm-ups code as nothing.  Codes
+                    // are ORed at absolute LDS bit addresses pa (word address (pa >> 5) * 4).
                     const uint32_t psz = 4096u >> o;
+                    const uint32_t img_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)img;
+                    // (one variant: a second, escape-free copy of the loop made the allocator spill)
+                    {
+                        constexpr bool E = true;
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const uint32_t p = pq4[q];
-                        const uint32_t i0 = l * 64u + 16u * q;
-                        part_header(p, i0 != 0 && (i0 & (psz - 1u)) == 0);
+                        for (int q = 0; q < 4; q++) {
+                            __builtin_amdgcn_sched_barrier(0);  // the group's constants live one group at a time
+                            const uint32_t p = pq4[q];
+                            const uint32_t i0 = l * 64u + 16u * q;
+                            part_header(p, i0 != 0 && (i0 & (psz - 1u)) == 0);
+                            const bool esc = (p & 0x80u) != 0;
+                            const uint32_t wb = p & 0x7Fu, pr = esc ? 0u : p;
+                            const uint32_t cl = esc ? wb : pr + 1u;
+                            const uint32_t cmask = esc ? ((1u << wb) - 1u) : ((1u << pr) - 1u);
+                            const uint32_t cbit = esc ? 0u : (1u << pr);
+                            const uint32_t ncl = 64u - cl;
+                            uint32_t pa = 8u * img_lds + pos;
 #pragma unroll
-                        for (int jj = 0; jj < 16; jj++) {
-                            const int j = 16 * q + jj;
-                            code((int32_t)s[j], p, j < KW && l == 0 && (uint32_t)j < k);
+                            for (int jj = 0; jj < 16; jj++) {
+                                const int j = 16 * q + jj;
+                                const bool warm = j < KW && l == 0 && (uint32_t)j < k;
+                                const int32_t r = (int32_t)s[j];
+                                const uint32_t zz = zigzag32(r);
+                                const uint32_t src = E ? (esc ? (uint32_t)r : zz) : zz;
+                                uint32_t v = (src & cmask) | cbit;
+                                uint32_t qz = E ? (esc ? 0u : (zz >> pr)) : (zz >> pr);
+                                uint32_t sh = ncl, adv = cl;
+                                if (j < KW) {
+                                    v = warm ? 0u : v;
+                                    qz = warm ? 0u : qz;
+                                    sh = warm ? 64u : sh;
+                                    adv = warm ? 0u : adv;
+                                }
+                                pa += qz;
+                                const uint64_t t = (uint64_t)v << ((sh - (pa & 31u)) & 63u);
+                                lds_or2((pa >> 3) & ~3u, (uint32_t)(t >> 32), (uint32_t)t);
+                                pa += adv;
+                            }
+                            pos = pa - 8u * img_lds;
                         }
                     }
                 } else {
@@ -2064,27 +2140,8 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         __syncthreads();
 
         STAMP(5);
-        // ---- 5. image -> out[D, D + fbytes): big-endian words realigned to the byte offset
-        {
-            const uint64_t E = D + fbytes;
-            const uint64_t q0 = D >> 2, q1 = (E + 3u) >> 2;
-            const uint32_t sa = (uint32_t)(D & 3u);
-            uint32_t *o32 = (uint32_t *)a.out;
-            for (uint64_t q = q0 + tid; q < q1; q += NT) {
-                const uint32_t m = (uint32_t)(q - q0);
-                const uint32_t lo = img[m];
-                const uint32_t hi = m ? img[m - 1u] : 0u;
-                const uint32_t v = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(hi, lo, sa) : lo);
-                const uint64_t b0 = 4u * q;
-                if (b0 >= D && b0 + 4u <= E) {
-                    o32[q] = v;
-                } else {
-#pragma unroll
-                    for (uint32_t b = 0; b < 4; b++)
-                        if (b0 + b >= D && b0 + b < E) a.out[b0 + b] = (uint8_t)(v >> (8 * b));
-                }
-            }
-        }
+        // ---- 5. image -> out[D, D + fbytes)
+        store_frame16(img, a.out, D, fbytes, tid, NT);
         // the image / staging area is reused by the next frame: with double buffering it is next
         // written by the DMA issued after the next frame's top barrier, which orders these reads
         // before it; synchronous staging refills it before that barrier

@@ -40,13 +40,6 @@ __device__ __forceinline__ void stage_dma_rot(const uint8_t *pcm, uint64_t off, 
     }
 }
 
-// OR two words into LDS at byte address addr (4-aligned) and addr + 4.  Inline asm: the
-// address is an absolute LDS address, so no base add per code; the ORs are ordered before
-// any read of the image by the lgkmcnt(0) of the next bar_lds().
-__device__ __forceinline__ void lds_or2(uint32_t addr, uint32_t hi, uint32_t lo) {
-    asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(addr), "v"(hi), "v"(lo) : "memory");
-}
-
 // dword offset of 4-sample group g of 16-sample chunk j in the rotated layout
 __device__ __forceinline__ uint32_t rot_off(uint32_t j, uint32_t g) { return 16u * j + 4u * ((g + (j >> 2)) & 3u); }
 
@@ -327,37 +320,8 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         bar_lds();
         STAMP(5);
 
-        // ---- 5. image -> out[D, D + fbytes): big-endian words realigned to the byte offset,
-        // 16 bytes per lane and store (edge units of the frame byte-masked)
-        {
-            const uint64_t E = D + fbytes;
-            const uint32_t sa = (uint32_t)(D & 3u);
-            const uint64_t qD = D >> 2;
-            for (uint64_t u = (D >> 4) + tid; u < ((E + 15u) >> 4); u += NT) {
-                const int32_t m0 = (int32_t)(4u * u - qD);  // image word of the unit's first word (>= -3)
-                uint32_t v[4];
-                uint32_t prev = m0 >= 1 ? img[m0 - 1] : 0u;
-#pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    const int32_t m = m0 + c;
-                    const uint32_t lo = m >= 0 ? img[m] : 0u;
-                    v[c] = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(prev, lo, sa) : lo);
-                    prev = lo;
-                }
-                const uint64_t b0 = 16u * u;
-                if (b0 >= D && b0 + 16u <= E) {
-                    *(uint4 *)(a.out + b0) = make_uint4(v[0], v[1], v[2], v[3]);
-                } else {
-#pragma unroll
-                    for (int c = 0; c < 4; c++)
-#pragma unroll
-                        for (uint32_t b = 0; b < 4; b++) {
-                            const uint64_t bb = b0 + 4u * c + b;
-                            if (bb >= D && bb < E) a.out[bb] = (uint8_t)(v[c] >> (8 * b));
-                        }
-                }
-            }
-        }
+        // ---- 5. image -> out[D, D + fbytes)
+        store_frame16(img, a.out, D, fbytes, tid, NT);
         // no barrier here: the image / staging area is next written by the DMA issued after the
         // next frame's top barrier, which already orders this frame's last reads before it
         STAMP(6);
