@@ -24,6 +24,11 @@ namespace fg {
 // compile-time value tag for uniform dispatch (one branch around a loop, not one per element)
 template <uint32_t V>
 using ic = std::integral_constant<uint32_t, V>;
+// type tag (C++17 has no std::type_identity)
+template <typename T>
+struct tyt {
+    using type = T;
+};
 
 // ------------------------------------------------------------------------
 // wave64 helpers
@@ -120,6 +125,10 @@ __device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
     v = row_or64(v);
     return rdl64(v, 0) | rdl64(v, 16) | rdl64(v, 32) | rdl64(v, 48);
+}
+__device__ __forceinline__ uint32_t wave_max32(uint32_t v) {
+    v = row_max32(v);
+    return max(max(rdl(v, 0), rdl(v, 16)), max(rdl(v, 32), rdl(v, 48)));
 }
 __device__ __forceinline__ uint32_t wave_xor32(uint32_t v) {
     v = row_xor32(v);
@@ -961,6 +970,42 @@ __device__ __forceinline__ void residuals_lpc_inplace(ST (&s)[64], const ST (&hs
     }
 }
 
+// Fast LPC residual pass (full frames, order <= W taps; c[t] = 0 past the order): the
+// prediction's low word P_lo = bits [shift+31 : shift] of the i64 sum, e = x - P_lo mod 2^32
+// (exact when the caller's magnitude bound holds).  Per 16-sample group g: S += |e|,
+// T |= e ^ (e >> 31) (= zz >> 1), N |= e (bit 31: some e < 0); lane 0's first `nwarm`
+// samples (warm-ups) are left out.
+template <int W, int LPWX>
+__device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int32_t (&hs)[LPWX], const int32_t (&c)[LPWX],
+                                              uint32_t shift, uint32_t nwarm, uint64_t (&S)[4], uint32_t (&T)[4],
+                                              uint32_t (&N)[4]) {
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        int64_t acc = 0;
+#pragma unroll
+        for (int t = 0; t < W; t++) {
+            const int idx = j - 1 - t;
+            const int32_t xv = idx >= 0 ? x[idx >= 0 ? idx : 0] : hs[(-idx - 1) >= 0 ? (-idx - 1) : 0];
+            acc += (int64_t)c[t] * (int64_t)xv;
+        }
+        const uint32_t plo = __builtin_amdgcn_alignbit((uint32_t)((uint64_t)acc >> 32), (uint32_t)acc, shift);
+        uint32_t e = (uint32_t)x[j] - plo;
+        const uint32_t sg = (uint32_t)((int32_t)e >> 31);
+        uint32_t t = e ^ sg;
+        uint32_t av = t - sg;
+        if (j < LPWX) {
+            const bool warm = (uint32_t)j < nwarm;
+            e = warm ? 0u : e;
+            t = warm ? 0u : t;
+            av = warm ? 0u : av;
+        }
+        S[j >> 4] += av;
+        T[j >> 4] |= t;
+        N[j >> 4] |= e;
+        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound the scheduler's hoisting
+    }
+}
+
 // ------------------------------------------------------------------------
 // Kernel 1: frame analysis.  One workgroup per frame (persistent loop), one
 // wave per candidate subframe.  Decides every candidate exactly as
@@ -1348,16 +1393,16 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 }
             }
         };
-        auto rice_search = [&](const SumT (&S8)[4], const uint32_t (&O8)[4], uint32_t kw, uint32_t P, uint8_t *pb,
-                               uint32_t &best_o, uint32_t &best_m) -> uint64_t {
+        // SWT: tyt<uint32_t> where every partition below order 0 sums < 2^32 (|e| <= 2^20), else tyt<uint64_t>
+        auto rice_search = [&](auto SWT, const auto (&S8)[4], const uint32_t (&O8)[4], uint32_t kw, uint32_t P,
+                               uint8_t *pb, uint32_t &best_o, uint32_t &best_m) -> uint64_t {
             uint64_t tots[9];
             uint32_t fives[9];
             if constexpr (FULL) {
                 uint32_t W8[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) W8[q] = bitlen32(O8[q]);
-                // 16-bit fixed prediction: every partition below order 0 sums < 2^32 (|e| <= 2^20)
-                using SW = typename std::conditional<(CLS == 16 && LPW == 0), uint32_t, uint64_t>::type;
+                using SW = typename decltype(SWT)::type;
                 const SW S7a = (SW)S8[0] + (SW)S8[1], S7b = (SW)S8[2] + (SW)S8[3];
                 const uint32_t W7a = max(W8[0], W8[1]), W7b = max(W8[2], W8[3]);
                 const SW S6 = S7a + S7b;
@@ -1491,6 +1536,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             return best;
         };
 
+        // 16-bit fixed prediction: every partition below order 0 sums < 2^32 (|e| <= 2^20)
+        using SWD = typename std::conditional<(CLS == 16 && LPW == 0), uint32_t, uint64_t>::type;
         // LPC mode (build-defined): estimates are whole payloads, warm-ups included
         const bool lpc_on = LPW > 0 && a.lpc_order != 0;
         uint32_t cur = 0;  // parameter buffer holding the current choice (LPC: 2 per wave)
@@ -1515,7 +1562,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
 
             // ---- 7. parameter search
             uint32_t best_o, best_m;
-            uint64_t best = rice_search(S8, O8, k, P, par, best_o, best_m);
+            uint64_t best = rice_search(tyt<SWD>{}, S8, O8, k, P, par, best_o, best_m);
             if (lpc_on) best += (uint64_t)k * bps;
 
             // ---- 8. FIXED iff its estimate < the verbatim estimate (encoder.zig:538)
@@ -1553,13 +1600,66 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     int32_t hs[LPW];
 #pragma unroll
                     for (int t = 0; t < LPW; t++) hs[t] = shr1(x[63 - t]);
+                    // fast path bound (full frames): |x| <= xmax for every sample of the wave
+                    uint32_t xmax = 0;
+                    if constexpr (FULL) {
+                        uint32_t xm = 0;
+#pragma unroll
+                        for (int j = 0; j < 64; j++) xm = max(xm, (uint32_t)(x[j] < 0 ? -(int64_t)x[j] : x[j]));
+                        xmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max32(xm));
+                    }
                     for (uint32_t q = 1; q <= Q; q++) {
                         const int32_t shq = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + 12u]);
                         if (shq < 0) continue;
                         int32_t c[LPW];
+                        uint64_t csum = 0;
 #pragma unroll
-                        for (int t = 0; t < LPW; t++)
+                        for (int t = 0; t < LPW; t++) {
                             c[t] = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + t]);
+                            csum += (uint64_t)(c[t] < 0 ? -c[t] : c[t]);
+                        }
+                        if constexpr (FULL) {
+                            // Fast path: |P| <= (csum * xmax >> shq) + 1 for the prediction P = acc >> shq,
+                            // so |e| = |x - P| < 3 * 2^30 when the test holds.  Then the low words
+                            // suffice: e_lo = x - P_lo (mod 2^32) and e is usable (e in [-2^30, 2^30))
+                            // iff e_lo ^ (e_lo >> 31) < 2^30 -- no 64-bit residual, no per-sample check.
+                            if ((uint64_t)xmax + ((csum * xmax) >> shq) + 1u < (3ull << 30)) {
+                                uint64_t S8[4] = {0, 0, 0, 0};
+                                uint32_t T8[4] = {0, 0, 0, 0}, N8[4] = {0, 0, 0, 0};
+                                const uint32_t nw = l == 0 ? q : 0u;
+                                if (q <= 4u) lpc_fast_pass<4, LPW>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
+                                else if (LPW <= 8 || q <= 8u) lpc_fast_pass<(LPW < 8 ? LPW : 8), LPW>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
+                                else lpc_fast_pass<LPW, LPW>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
+                                const uint32_t tall = (uint32_t)__builtin_amdgcn_readfirstlane(
+                                    (int)wave_or32(T8[0] | T8[1] | T8[2] | T8[3]));
+                                if (tall >= (1u << 30)) continue;  // some residual outside [-2^30, 2^30)
+                                // OR of the zigzags' bit lengths: zz = 2t + sign
+                                uint32_t O8[4];
+#pragma unroll
+                                for (int g = 0; g < 4; g++) O8[g] = T8[g] ? ((T8[g] << 1) | 1u) : (N8[g] >> 31);
+                                const uint32_t P = part_cap(q);
+                                uint8_t *pb = par + (cur ^ 1u) * 512u;
+                                uint32_t best_o, best_m;
+                                uint64_t rb;
+                                if (tall < (1u << 20)) {  // |e| <= 2^20: 32-bit partition sums
+                                    const uint32_t S32[4] = {(uint32_t)S8[0], (uint32_t)S8[1], (uint32_t)S8[2], (uint32_t)S8[3]};
+                                    rb = rice_search(tyt<uint32_t>{}, S32, O8, q, P, pb, best_o, best_m);
+                                } else {
+                                    rb = rice_search(tyt<uint64_t>{}, S8, O8, q, P, pb, best_o, best_m);
+                                }
+                                const uint64_t tot = rb + (uint64_t)q * (bps + (uint32_t)kLpcPrec) + 9u;
+                                if (tot < R.est) {
+                                    R.type = 3;
+                                    R.est = tot;
+                                    R.order = q;
+                                    R.porder = best_o;
+                                    R.method = best_m;
+                                    R.lsh = shq;
+                                    cur ^= 1u;
+                                }
+                                continue;
+                            }
+                        }
                         SumT S8[4] = {0, 0, 0, 0};
                         uint32_t O8[4] = {0, 0, 0, 0};
                         const uint32_t P = part_cap(q);
@@ -1576,7 +1676,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                         if (__any(bad)) continue;
                         uint8_t *pb = par + (cur ^ 1u) * 512u;
                         uint32_t best_o, best_m;
-                        const uint64_t rb = rice_search(S8, O8, q, P, pb, best_o, best_m);
+                        const uint64_t rb = rice_search(tyt<SumT>{}, S8, O8, q, P, pb, best_o, best_m);
                         const uint64_t tot = rb + (uint64_t)q * (bps + (uint32_t)kLpcPrec) + 9u;
                         if (tot < R.est) {
                             R.type = 3;
