@@ -422,8 +422,25 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         c->nt_pack4 = 512u;
         if (const char *e = std::getenv("FLACGPU_PACK4")) c->nt_pack4 = e[0] == '0' ? 0u : 512u;  // A/B knob
     }
+    bool packw_dbuf = true;
+    // k_packw (fg_packw.hpp) where k_pack's occupancy is poor: 32-bit samples (i64 lanes, 2 waves
+    // per SIMD) or more than two written subframes (one workgroup per CU).  Mono/stereo 8-24-bit
+    // frames stay on k_pack: its small single-buffered workgroups keep 4-5 frames in flight per
+    // CU, which measured faster (c3 pack alone: 1.26 ms vs 1.40-1.66 ms for the packw variants).
+    bool use_packw = c->B == 4u || n_out > 2u;
+    if (const char *e = std::getenv("FLACGPU_PACKW")) use_packw = e[0] == '1' ? true : (e[0] == '0' ? false : use_packw);  // A/B knob
+    if (!c->nt_pack4 && use_packw) {
+        // WPS waves per written subframe, 16 (<= 4 subframes) or 32 samples per lane;
+        // double-buffered staging where two workgroups per CU still fit
+        uint32_t wps = n_out <= 4u ? 4u : 2u;
+        if (const char *e = std::getenv("FLACGPU_PACKW_WPS")) wps = (e[0] == '2' && n_out <= 8u) ? 2u : wps;  // tuning knob
+        c->nt_pack4 = 64u * n_out * wps;
+        packw_dbuf = pack_layout(c->C, c->B, c->image_bytes, true).total * 2u <= 160u * 1024u;
+        if (const char *e = std::getenv("FLACGPU_PACKW_DBUF")) packw_dbuf = packw_dbuf && e[0] == '1';  // tuning knob
+        c->pack_dbuf = packw_dbuf;  // k_pack then runs tail frames only (never double-buffered)
+    }
     if (c->nt_pack4) {
-        c->lds_pack4 = pack_layout(c->C, c->B, c->image_bytes, true).total;
+        c->lds_pack4 = pack_layout(c->C, c->B, c->image_bytes, packw_dbuf).total;
         c->crc_hmax4 = ((c->image_bytes / 4u + 2u * c->nt_pack4 - 1u) / (2u * c->nt_pack4)) | 1u;
     }
     if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u ||

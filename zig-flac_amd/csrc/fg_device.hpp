@@ -853,50 +853,64 @@ __device__ __forceinline__ void lpc_autocorr(const ST (&s)[64], uint32_t n, uint
     for (int g = 0; g <= W; g++) R[g] = (int64_t)wave_sum64((uint64_t)acc[g]);
 }
 
-// Levinson-Durbin + quantisation of every order 1..Q (all lanes compute the same
-// values; lane `writer` stores them): tab[(q-1)*13 + t] = coefficient t of order q
-// (0 past q), tab[(q-1)*13 + 12] = its shift, or -1 if the order is unusable.
+// Levinson-Durbin + quantisation of every order 1..Q: tab[(q-1)*13 + t] = coefficient t of
+// order q (0 past q), tab[(q-1)*13 + 12] = its shift, or -1 if the order is unusable.  The
+// recursion is serial and runs on every lane; lane m keeps the coefficients of order m+1 as
+// they are produced and quantises them itself afterwards (each order's error-feedback chain
+// is independent), so the quantisation costs one order's chain, not all of them in series.
 template <int W>
-__device__ __forceinline__ void lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q, int32_t *tab, bool writer) {
+__device__ __forceinline__ void lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q, int32_t *tab, uint32_t lane) {
 #pragma clang fp contract(off)
-    if (writer)
-        for (uint32_t q = 0; q < (uint32_t)kLpcMax; q++) tab[q * 13u + 12u] = -1;
-    double r[W + 1], a[W], tmp[W];
+    double r[W + 1], a[W], tmp[W], mine[W];
 #pragma unroll
     for (int i = 0; i <= W; i++) r[i] = (double)R[i];
-    if (!(r[0] > 0.0)) return;
-    double err = r[0];
-    bool live = true;  // uniform: order m+1 is computed while live (stops at Q or when err <= 0)
 #pragma unroll
-    for (int m = 0; m < W; m++) {
-        live = live && (uint32_t)m < Q;
-        if (!live) continue;
-        double acc = r[m + 1];
+    for (int t = 0; t < W; t++) mine[t] = 0.0;
+    bool have = false;  // this lane's order (lane + 1) was reached
+    if (r[0] > 0.0) {
+        double err = r[0];
+        bool live = true;  // uniform: order m+1 is computed while live (stops at Q or when err <= 0)
 #pragma unroll
-        for (int t = 0; t < m; t++) {
-            const double p = a[t] * r[m - t];
-            acc = acc - p;
+        for (int m = 0; m < W; m++) {
+            live = live && (uint32_t)m < Q;
+            if (!live) continue;
+            double acc = r[m + 1];
+#pragma unroll
+            for (int t = 0; t < m; t++) {
+                const double p = a[t] * r[m - t];
+                acc = acc - p;
+            }
+            const double k = acc / err;
+#pragma unroll
+            for (int t = 0; t < m; t++) {
+                const double p = k * a[m - 1 - t];
+                tmp[t] = a[t] - p;
+            }
+#pragma unroll
+            for (int t = 0; t < m; t++) a[t] = tmp[t];
+            a[m] = k;
+            const bool me = lane == (uint32_t)m;
+            have = have || me;
+#pragma unroll
+            for (int t = 0; t <= m; t++) mine[t] = me ? a[t] : mine[t];
+            const double kk = k * k;
+            err = err * (1.0 - kk);
+            live = err > 0.0;
         }
-        const double k = acc / err;
+    }
+    // quantise order lane+1 (oracle_lpc_quantize); lanes past W or past the recursion keep -1
+    const uint32_t m = lane;
+    int32_t shq = -1;
+    int32_t qc[W];
 #pragma unroll
-        for (int t = 0; t < m; t++) {
-            const double p = k * a[m - 1 - t];
-            tmp[t] = a[t] - p;
-        }
-#pragma unroll
-        for (int t = 0; t < m; t++) a[t] = tmp[t];
-        a[m] = k;
-        // quantise order m+1 (oracle_lpc_quantize)
+    for (int t = 0; t < W; t++) qc[t] = 0;
+    if (have) {
         double cmax = 0.0;
 #pragma unroll
-        for (int t = 0; t <= m; t++) {
-            const double v = a[t] < 0.0 ? -a[t] : a[t];
-            cmax = v > cmax ? v : cmax;
+        for (int t = 0; t < W; t++) {
+            const double v = mine[t] < 0.0 ? -mine[t] : mine[t];
+            cmax = ((uint32_t)t <= m && v > cmax) ? v : cmax;
         }
-        int32_t shq = -1;
-        int32_t qc[W];
-#pragma unroll
-        for (int t = 0; t < W; t++) qc[t] = 0;
         if (cmax > 0.0) {
             int e;
             (void)frexp(cmax, &e);
@@ -907,24 +921,23 @@ __device__ __forceinline__ void lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q,
                 const int64_t qmax = (1ll << (kLpcPrec - 1)) - 1, qmin = -(1ll << (kLpcPrec - 1));
                 double carry = 0.0;
 #pragma unroll
-                for (int t = 0; t <= m; t++) {
-                    double v = a[t] * scale;
-                    v = v + carry;
-                    int64_t qi = v >= 0.0 ? (int64_t)floor(v + 0.5) : -(int64_t)floor(-v + 0.5);
-                    qi = qi > qmax ? qmax : (qi < qmin ? qmin : qi);
-                    carry = v - (double)qi;
-                    qc[t] = (int32_t)qi;
+                for (int t = 0; t < W; t++) {
+                    if ((uint32_t)t <= m) {
+                        double v = mine[t] * scale;
+                        v = v + carry;
+                        int64_t qi = v >= 0.0 ? (int64_t)floor(v + 0.5) : -(int64_t)floor(-v + 0.5);
+                        qi = qi > qmax ? qmax : (qi < qmin ? qmin : qi);
+                        carry = v - (double)qi;
+                        qc[t] = (int32_t)qi;
+                    }
                 }
             }
         }
-        if (writer) {
+    }
+    if (lane < (uint32_t)kLpcMax) {
 #pragma unroll
-            for (int t = 0; t < kLpcMax; t++) tab[m * 13 + t] = (t < W) ? qc[t < W ? t : 0] : 0;
-            tab[m * 13 + 12] = shq;
-        }
-        const double kk = k * k;
-        err = err * (1.0 - kk);
-        live = err > 0.0;
+        for (int t = 0; t < kLpcMax; t++) tab[m * 13u + t] = (t < W) ? qc[t < W ? t : 0] : 0;
+        tab[m * 13u + 12u] = shq;
     }
 }
 
@@ -1435,7 +1448,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 const uint32_t m0 = rdl(Wl[3], 0), m1 = rdl(Wl[3], 16), m2 = rdl(Wl[3], 32), m3 = rdl(Wl[3], 48);
 #pragma unroll
                 for (int o = 0; o < 9; o++) {
-                    if ((uint32_t)o <= P) {
+                    if (true) {  // every order unconditionally: straight-line code the scheduler can interleave (o > P is never selected)
                         uint32_t cost = 0, c;
                         bool five = false;
                         if (o >= 6) {
@@ -1589,7 +1602,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                         int64_t Rac[LPW + 1];
                         lpc_autocorr<LPW, int32_t>(x, n, l, Rac);
                         __builtin_amdgcn_sched_barrier(0);
-                        lpc_coefs<LPW>(Rac, Q, ltab, l == 0);
+                        lpc_coefs<LPW>(Rac, Q, ltab, l);
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2256,6 +2269,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
 }
 
 #include "fg_pack4.hpp"
+#include "fg_packw.hpp"
 
 // persistent launch: grid = min(frames, resident workgroups)
 template <typename KernelT>
@@ -2307,6 +2321,16 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
         // full 16-bit two-channel frames: four waves per written subframe (fg_pack4.hpp)
         if (stage == 1 && full && a.channels == 2 && threads == 512u)
             return launch_persistent(k_pack4<512>, a, threads, lds, st);
+    }
+    // other full frames: WPS waves per written subframe (fg_packw.hpp); the host marks it by
+    // the thread count 64 * n_out * WPS (k_pack runs 64 * n_out)
+    if (stage == 1 && full) {
+        const uint32_t n_out = a.stereo ? 2u : a.channels;
+        if (threads == 64u * n_out * 4u) {
+            if (a.channels == 2) return launch_persistent(k_packw<B, CLS, 2, LPW, 16>, a, threads, lds, st);
+            return launch_persistent(k_packw<B, CLS, 0, LPW, 16>, a, threads, lds, st);
+        }
+        if (threads == 64u * n_out * 2u) return launch_persistent(k_packw<B, CLS, 0, LPW, 32>, a, threads, lds, st);
     }
     if (a.channels == 2) FG_L(2, 256);
     if (a.channels == 1) FG_L(1, 256);

@@ -1,0 +1,350 @@
+// fg_packw.hpp -- frame packing with several waves per written subframe for every full-frame
+// configuration k_pack4 does not cover: 24/32-bit samples, mono and multichannel streams,
+// LPC subframes (included by fg_device.hpp inside namespace fg).
+//
+// k_pack gives each written subframe one wave of 64-sample lanes: one dependent chain of 64
+// codes per lane, and for 8 channels only 8 waves per CU (the 96 KiB staging admits one
+// workgroup).  Here WPS = 64 / SPL waves share a subframe and a lane owns SPL (16 or 32)
+// consecutive samples: wave w packs part hq = w % WPS of written subframe w / WPS.  Per frame
+// (frame_writer.zig:269-372 restated):
+//   1. the lane loads its SPL samples and the KH before them (fixed: 4, LPC: the taps) of its
+//      candidate from the staged PCM (encoder.zig:329-350), applies the waste shift and the
+//      predictor of the descriptor (fixed.zig:30-81; LPC: the build-defined contract, §4b);
+//   2. code lengths -> a wave prefix scan on top of the part's base, which is the prefix of the
+//      analysis kernel's exact 64-sample segment lengths;
+//   3. branch-free code emission into the zeroed LDS frame image, CRC-16 (one chain per thread,
+//      one shift multiply), 16-byte stores at the frame's final byte offset.
+#pragma once
+
+// Sample i of channel c of the staged frame (padded layout, fg_layout.hpp), sign-extended.
+template <int B>
+__device__ __forceinline__ int32_t staged_sample(const uint32_t *stg, uint32_t cst, uint32_t CB, uint32_t i, uint32_t c) {
+    const uint32_t byte = (i >> 6) * cst * 4u + (i & 63u) * CB + c * (uint32_t)B;
+    if constexpr (B == 4) {
+        return (int32_t)stg[byte >> 2];
+    } else if constexpr (B == 3) {
+        const uint32_t wd = byte >> 2, o = byte & 3u;
+        const uint32_t v = __builtin_amdgcn_alignbyte(stg[wd + 1u], stg[wd], o);
+        return (int32_t)(v << 8) >> 8;
+    } else if constexpr (B == 2) {
+        const uint32_t v = stg[byte >> 2];
+        return (int32_t)((byte & 2u) ? v : (v << 16)) >> 16;
+    } else {
+        const uint32_t v = stg[byte >> 2];
+        return (int32_t)(v << (24u - 8u * (byte & 3u))) >> 24;
+    }
+}
+
+template <int B, int CLS, int NC, int LPW, int SPL>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8))) k_packw(EncodeArgs a) {
+    using ST = typename Cls<CLS>::S;
+    constexpr int KH = LPW > 4 ? LPW : 4;  // history samples (most warm-ups of any predictor)
+    constexpr uint32_t WPS = 64u / SPL;     // waves per written subframe
+    constexpr int NG = SPL / 16;            // 16-sample groups per lane (one Rice partition each)
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+    const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l0 = lane_id();
+    const uint32_t sfi = wave / WPS, hq = wave % WPS;  // written subframe, part
+    const uint32_t C = NC ? (uint32_t)NC : a.channels;
+    const uint32_t CB = C * (uint32_t)B;
+    const uint32_t cw = 16u * C * B, cst = cw + stage_pad(C, B);
+    const bool dbuf = a.pack_dbuf != 0;
+    const PackLayout LY = pack_layout(C, B, a.image_bytes, dbuf);
+    uint16_t *crct = (uint16_t *)(smem + LY.crc);
+    uint32_t *misc = (uint32_t *)(smem + LY.misc);
+    for (uint32_t i = tid; i < 2048u; i += NT) crct[i] = a.crc_tab[i];
+    const bool stereo = a.stereo != 0;
+
+    uint32_t *ctr = a.work_ctr + 2u;
+    if (blockIdx.x == 0 && tid == 0) a.work_ctr[0] = a.work_ctr[1] = 0u;  // the analysis kernel's queues
+    if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
+    __syncthreads();
+    uint32_t jidx = blockIdx.x, buf = 0;
+    uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
+    FrameJob job{}, jn{};
+    if (jidx < a.n_jobs) job = a.jobs[jidx];
+    if (nxt < a.n_jobs) jn = a.jobs[nxt];
+    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, wave, NW, l0);
+    while (jidx < a.n_jobs) {
+        const uint32_t l = opaque(l0);
+        if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
+        uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
+        uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
+        const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
+        const FrameDesc *F = (const FrameDesc *)fd;
+        const SubDesc *sd0 = (const SubDesc *)(fd + sizeof(FrameDesc));
+        const SubDesc *sd = sd0 + sfi;
+        const uint32_t total_bits = F->total_bits;
+        const uint32_t fbytes = ((total_bits + 7u) >> 3) + 2u;
+        const uint64_t D = a.offsets[job.slot];
+        const uint32_t Lb = (total_bits + 7u) >> 3;
+        const uint32_t W4 = Lb >> 2;
+        const uint32_t H = max((W4 + 2u * NT - 1u) / (2u * NT), 1u);  // words per thread / 2
+        const uint32_t hcq = min(H, a.crc_hmax4) - 1u;
+        const uint32_t crc_pw = a.crc_pow4[hcq * NT + tid];
+        const bool skip = fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap;  // uniform
+        const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
+                       method = sd->method, cand = sd->cand;
+        const uint32_t i0 = hq * 64u * SPL + SPL * l0;  // first sample of this lane
+        uint32_t pq[NG];
+#pragma unroll
+        for (int g = 0; g < NG; g++) pq[g] = sd->params[(i0 + 16u * g) >> (12u - o)];
+        const uint32_t lb = sd->lane_bits[l0];
+        uint32_t sub_start = 8u * F->hdr_bytes;
+        for (uint32_t t = 0; t < sfi; t++) sub_start += sd0[t].bits;
+
+        // ---- 1. PCM (double-buffered: DMA'd during the previous frame) -> samples
+        if (dbuf) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            stage_dma(a.pcm, job.pcm_off, stg, cw, cst, wave, NW, l);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        if (dbuf && nxt < a.n_jobs) stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, wave, NW, l);
+        FrameJob jnn{};
+        if (nn < a.n_jobs) jnn = a.jobs[nn];
+        if (skip) {
+            if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
+            __syncthreads();
+            jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
+            continue;
+        }
+        // x[KH + j] = sample i0 + j of the candidate, x[KH - 1 - t] = sample i0 - 1 - t (0 before
+        // the subframe: only lane 0 of part 0, whose first k samples are warm-ups)
+        ST x[KH + SPL];
+        {
+            const uint32_t ia = SPL * l + hq * 64u * SPL;  // == i0, from the opaque lane id
+            const uint32_t kind = stereo ? cand : 0u;        // 0 plain channel, 1 R, 2 mid, 3 side
+            const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand;
+            auto fill = [&](auto KD) {
+                constexpr uint32_t KND = decltype(KD)::value;
+#pragma unroll
+                for (int j = 0; j < KH + SPL; j++) {
+                    const bool before = j < KH && ia + (uint32_t)j < (uint32_t)KH;  // sample index < 0
+                    const uint32_t i = before ? 0u : ia + (uint32_t)j - (uint32_t)KH;
+                    int64_t v;
+                    if constexpr (KND <= 1) {
+                        v = staged_sample<B>(stg, cst, CB, i, chan);
+                    } else {
+                        const int64_t L = staged_sample<B>(stg, cst, CB, i, 0u), R = staged_sample<B>(stg, cst, CB, i, 1u);
+                        v = KND == 2 ? (L + R) >> 1 : L - R;
+                    }
+                    x[j] = before ? (ST)0 : (ST)v;
+                    if ((j & 15) == 15) __builtin_amdgcn_sched_barrier(0);
+                }
+            };
+            if (kind <= 1) fill(ic<0>{});
+            else if (kind == 2) fill(ic<2>{});
+            else fill(ic<3>{});
+        }
+        // lane offsets: the part's base = the analysis kernel's segment lengths before it
+        const uint32_t lbs = wave_incl_scan32(lb);
+        const uint32_t qbase = hq ? rdl(lbs, (int)(SPL * hq - 1u)) : 0u;
+        bar_lds();  // staging dead: zero the image
+        const uint32_t Wz = (fbytes + 3u) / 4u + 2u;
+        for (uint32_t i = tid; i < Wz; i += NT) img[i] = 0;
+
+        // ---- 2. waste shift and residuals, lengths of this lane's codes
+        const uint32_t bps = bd - w;
+        if (type != 0 && w != 0) {
+#pragma unroll
+            for (int j = 0; j < KH + SPL; j++) x[j] >>= w;
+        }
+        const bool first = (hq == 0) && (l == 0);
+        const uint32_t param_len = 4u + method;
+        uint32_t r[SPL];
+        if (type == 2) {
+            auto fixed = [&](auto KO) {
+                constexpr int K = (int)decltype(KO)::value;
+#pragma unroll
+                for (int j = 0; j < SPL; j++) {
+                    ST q1 = x[KH + j - 1], q2 = x[KH + j - 2], q3 = x[KH + j - 3], q4 = x[KH + j - 4];
+                    r[j] = (uint32_t)(int32_t)fixed_residual<K, ST>(x[KH + j], q1, q2, q3, q4);
+                }
+            };
+            if (k == 0) fixed(ic<0>{});
+            else if (k == 1) fixed(ic<1>{});
+            else if (k == 2) fixed(ic<2>{});
+            else if (k == 3) fixed(ic<3>{});
+            else fixed(ic<4>{});
+        } else if (LPW > 0 && type == 3) {
+            if constexpr (LPW > 0) {
+                int32_t c[LPW];
+#pragma unroll
+                for (int t = 0; t < LPW; t++) c[t] = __builtin_amdgcn_readfirstlane((int32_t)sd->coef[t < kLpcMax ? t : 0]);
+                const uint32_t shift = (uint32_t)(int32_t)sd->lpc_shift;
+#pragma unroll
+                for (int j = 0; j < SPL; j++) {
+                    int64_t acc = 0;
+#pragma unroll
+                    for (int t = 0; t < LPW; t++) acc += (int64_t)c[t] * (int64_t)x[KH + j - 1 - t];
+                    r[j] = (uint32_t)(int32_t)((int64_t)x[KH + j] - (acc >> shift));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < SPL; j++) r[j] = (uint32_t)(int32_t)x[KH + j];
+        }
+        // per 16-sample group the code shape is lane-constant (see k_pack4): rice = q zeros then
+        // (1 << p) | low p bits in p + 1 bits, escape = the raw wb-bit value; warm-ups (the
+        // subframe's first k samples, lane 0 of part 0) are written by the header writer
+        const uint32_t nwarm = (first && type >= 2) ? k : 0u;
+        auto warm_at = [&](int j) -> bool { return j < KH && (uint32_t)j < nwarm; };
+        uint32_t len = 0;
+        if (first) {
+            const uint32_t p0 = pq[0];
+            if (type == 0) len = 8u + bd;
+            else if (type == 1) len = 8u + w;
+            else len = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u) +
+                       (type == 3 ? 4u + 5u + k * sd->lpc_prec : 0u);
+        }
+        if (type == 1) {
+            len += SPL * bps;
+        } else if (type >= 2) {
+            const uint32_t psz = 4096u >> o;
+#pragma unroll
+            for (int g = 0; g < NG; g++) {
+                const uint32_t p = pq[g], ig = i0 + 16u * g;
+                const bool esc = (p & 0x80u) != 0;
+                const uint32_t pr = esc ? 0u : p, cl = esc ? (p & 0x7Fu) : pr + 1u;
+                if (ig != 0 && (ig & (psz - 1u)) == 0) len += param_len + (esc ? 5u : 0u);
+                uint32_t qs = 0, nc = 16;
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    const int j = 16 * g + jj;
+                    const uint32_t qz = zigzag32((int32_t)r[j]) >> pr;
+                    const bool wm = warm_at(j);
+                    qs = add_chain(qs, wm ? 0u : qz);
+                    if (j < KH) nc -= wm ? 1u : 0u;
+                }
+                len += (esc ? 0u : qs) + nc * cl;
+            }
+        }
+        const uint32_t lane_off = wave_incl_scan32(len) - len;
+        bar_lds();  // image zeroed
+        if (tid < 4) {
+            const uint32_t hv = F->hdr[tid];
+            if (hv) atomicOr(&img[tid], hv);
+        }
+
+        // ---- 3. pack: each lane ORs its codes into the image at its bit offset
+        {
+            uint32_t pos = sub_start + qbase + lane_off;
+            const uint64_t mask = ~0ull >> (64 - (bps ? bps : 1u));
+            if (first) {
+                AtomicWriter bw;
+                bw.init(img, pos);
+                if (type == 0) {  // writeConstantSubframe: 0x00, value << waste in bd bits
+                    bw.put(0, 8);
+                    bw.put(((uint64_t)sd->cval << w) & (~0ull >> (64 - bd)), bd);
+                } else {
+                    // type code: VERBATIM 1, FIXED 8|k, LPC 0x20|(k-1) (build-defined)
+                    const uint32_t tc = (type == 1) ? 1u : (type == 2 ? (8u | k) : (0x20u | (k - 1u)));
+                    bw.put((tc << 1) | (w ? 1u : 0u), 8);
+                    if (w) bw.put(1, w);
+                    if (type >= 2) {
+#pragma unroll
+                        for (int j = 0; j < KH; j++)  // warm-up samples
+                            if ((uint32_t)j < k) bw.put((uint64_t)(int64_t)x[KH + j] & mask, bps);
+                        if (type == 3) {
+                            const uint32_t prec = sd->lpc_prec;
+                            bw.put(prec - 1u, 4);
+                            bw.put((uint32_t)(int32_t)sd->lpc_shift & 31u, 5);
+                            for (uint32_t t = 0; t < k; t++)
+                                bw.put((uint64_t)(int64_t)sd->coef[t] & (~0ull >> (64 - prec)), prec);
+                        }
+                        bw.put((method << 4) | o, 6);
+                        const uint32_t p0 = pq[0];
+                        if (p0 & 0x80u) {
+                            bw.put(0x0Fu | (method << 4), 4u + method);
+                            bw.put(p0 & 0x7Fu, 5);
+                        } else {
+                            bw.put(p0, 4u + method);
+                        }
+                    }
+                }
+                pos = bw.pos;
+            }
+            if (type == 1) {  // verbatim: the (waste-shifted) samples, up to 33 bits (32-bit side)
+#pragma unroll
+                for (int j = 0; j < SPL; j++) {
+                    put_or2(img, pos, (uint64_t)(int64_t)x[KH + j] & mask, bps);
+                    pos += bps;
+                }
+            } else if (type >= 2) {
+                const uint32_t psz = 4096u >> o;
+                const uint32_t esc_code = (0x0Fu | (method << 4)) << 5;
+                const uint32_t img_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)img;
+#pragma unroll
+                for (int g = 0; g < NG; g++) {
+                    __builtin_amdgcn_sched_barrier(0);  // the group's constants live one group at a time
+                    const uint32_t p = pq[g], ig = i0 + 16u * g;
+                    const bool esc = (p & 0x80u) != 0;
+                    const uint32_t wb = p & 0x7Fu, pr = esc ? 0u : p;
+                    if (ig != 0 && (ig & (psz - 1u)) == 0) {  // partition header
+                        const uint32_t hl = param_len + (esc ? 5u : 0u);
+                        put_or2(img, pos, esc ? (esc_code | wb) : p, hl);
+                        pos += hl;
+                    }
+                    const uint32_t cl = esc ? wb : pr + 1u;
+                    const uint32_t cmask = esc ? ((1u << wb) - 1u) : ((1u << pr) - 1u);  // wb <= 31
+                    const uint32_t cbit = esc ? 0u : (1u << pr);
+                    const uint32_t ncl = 64u - cl;
+                    uint32_t pa = 8u * img_lds + pos;
+#pragma unroll
+                    for (int jj = 0; jj < 16; jj++) {
+                        const int j = 16 * g + jj;
+                        const bool warm = warm_at(j);
+                        const uint32_t zz = zigzag32((int32_t)r[j]);
+                        uint32_t v = ((esc ? r[j] : zz) & cmask) | cbit;
+                        uint32_t qz = esc ? 0u : (zz >> pr);
+                        uint32_t sh = ncl, adv = cl;
+                        if (j < KH) {
+                            v = warm ? 0u : v;
+                            qz = warm ? 0u : qz;
+                            sh = warm ? 64u : sh;
+                            adv = warm ? 0u : adv;
+                        }
+                        pa += qz;
+                        const uint64_t t = (uint64_t)v << ((sh - (pa & 31u)) & 63u);
+                        lds_or2((pa >> 3) & ~3u, (uint32_t)(t >> 32), (uint32_t)t);
+                        pa += adv;
+                    }
+                    pos = pa - 8u * img_lds;
+                }
+            }
+        }
+        bar_lds();
+
+        // ---- 4. CRC-16 of the frame (one chain of 2H words per thread, see k_pack4)
+        {
+            const int32_t Z = (int32_t)(NT * 2u * H) - (int32_t)W4;
+            uint32_t ca = 0;
+            const int32_t va = (int32_t)(tid * 2u * H) - Z;
+            auto word = [&](int32_t rr) -> uint32_t { return rr >= 0 ? img[rr] : 0u; };
+            for (uint32_t i = 0; i < 2u * H; i += 2u)
+                ca = crc_word2(ca, word(va + (int32_t)i), word(va + (int32_t)i + 1), crct);
+            uint32_t contrib = crc_mulmod_t(ca, crc_pw, crct);
+            contrib = wave_xor32(contrib);
+            if (l == 0) misc[wave] = contrib;
+        }
+        bar_lds();
+        if (tid == 0) {
+            uint32_t crc = 0;
+            for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
+            for (uint32_t b = W4 * 4u; b < Lb; b++)
+                crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+            put_bits(img, Lb * 8u, crc, 16);
+        }
+        bar_lds();
+
+        // ---- 5. image -> out[D, D + fbytes)
+        store_frame16(img, a.out, D, fbytes, tid, NT);
+        // single buffer: the next frame's staging overwrites the image
+        if (!dbuf) __syncthreads();
+        jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
+    }  // persistent frame loop
+}
