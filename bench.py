@@ -566,7 +566,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "limiter": LIMITER[dom],
-                "kernel": {"analyze": "k_analyze (4096-sample frames)", "pack": "k_pack4 / k_pack",
+                "kernel": {"analyze": "k_analyze (4096-sample frames)", "pack": "k_pack4 / k_packw / k_pack",
                            "md5": "k_md5_streams"}[dom],
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,

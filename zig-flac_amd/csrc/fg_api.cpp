@@ -435,12 +435,13 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         uint32_t wps = n_out <= 4u ? 4u : 2u;
         if (const char *e = std::getenv("FLACGPU_PACKW_WPS")) wps = (e[0] == '2' && n_out <= 8u) ? 2u : wps;  // tuning knob
         c->nt_pack4 = 64u * n_out * wps;
-        packw_dbuf = pack_layout(c->C, c->B, c->image_bytes, true).total * 2u <= 160u * 1024u;
+        packw_dbuf = packw_layout(c->C, c->B, wps, c->image_bytes, true).total * 2u <= 160u * 1024u;
         if (const char *e = std::getenv("FLACGPU_PACKW_DBUF")) packw_dbuf = packw_dbuf && e[0] == '1';  // tuning knob
         c->pack_dbuf = packw_dbuf;  // k_pack then runs tail frames only (never double-buffered)
     }
     if (c->nt_pack4) {
-        c->lds_pack4 = pack_layout(c->C, c->B, c->image_bytes, packw_dbuf).total;
+        c->lds_pack4 = (c->C == 2 && c->B == 2 && !lpc) ? pack_layout(c->C, c->B, c->image_bytes, true).total
+                                                         : packw_layout(c->C, c->B, c->nt_pack4 / (64u * n_out), c->image_bytes, packw_dbuf).total;
         c->crc_hmax4 = ((c->image_bytes / 4u + 2u * c->nt_pack4 - 1u) / (2u * c->nt_pack4)) | 1u;
     }
     if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u ||

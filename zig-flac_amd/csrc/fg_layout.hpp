@@ -90,6 +90,24 @@ __host__ __device__ inline PackLayout pack_layout(uint32_t C, uint32_t B, uint32
     return L;
 }
 
+// k_packw staging (fg_packw.hpp): 64 chunks of 64 samples, each split into WPS sub-chunks of
+// 64 / WPS samples (one lane's samples) followed by one pad word each, so the WPS lanes that read
+// one chunk start in different banks (with the plain pad they would all hit one: a sub-chunk of
+// 16 or 32 samples is a multiple of 32 words for 8-byte and 24-byte sample rows).
+__host__ __device__ inline uint32_t packw_cst(uint32_t C, uint32_t B, uint32_t wps) { return 16u * C * B + wps; }
+__host__ __device__ inline PackLayout packw_layout(uint32_t C, uint32_t B, uint32_t wps, uint32_t image_bytes, bool dbuf) {
+    PackLayout L;
+    uint32_t r0 = 64u * packw_cst(C, B, wps) * 4u;
+    if (image_bytes > r0) r0 = image_bytes;
+    r0 = fg_round16(r0);
+    L.buf0 = 0;
+    L.buf1 = dbuf ? r0 : 0u;
+    L.crc = dbuf ? 2u * r0 : r0;
+    L.misc = L.crc + 4096u;
+    L.total = fg_round16(L.misc + 256u);
+    return L;
+}
+
 // Upper bound (bytes) of one encoded frame, block n <= 4096:
 // header <= 16 B; per subframe <= 14 + 4*bd + n*bd + n/2 bits (a FIXED subframe
 // is chosen only when its estimate < n*bps', and the exact Rice length exceeds

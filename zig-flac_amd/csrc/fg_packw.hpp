@@ -16,10 +16,9 @@
 //      one shift multiply), 16-byte stores at the frame's final byte offset.
 #pragma once
 
-// Sample i of channel c of the staged frame (padded layout, fg_layout.hpp), sign-extended.
+// Sample at byte `byte` of the staged frame, sign-extended.
 template <int B>
-__device__ __forceinline__ int32_t staged_sample(const uint32_t *stg, uint32_t cst, uint32_t CB, uint32_t i, uint32_t c) {
-    const uint32_t byte = (i >> 6) * cst * 4u + (i & 63u) * CB + c * (uint32_t)B;
+__device__ __forceinline__ int32_t staged_at(const uint32_t *stg, uint32_t byte) {
     if constexpr (B == 4) {
         return (int32_t)stg[byte >> 2];
     } else if constexpr (B == 3) {
@@ -32,6 +31,32 @@ __device__ __forceinline__ int32_t staged_sample(const uint32_t *stg, uint32_t c
     } else {
         const uint32_t v = stg[byte >> 2];
         return (int32_t)(v << (24u - 8u * (byte & 3u))) >> 24;
+    }
+}
+
+// Byte of sample i, channel c in the k_packw staging (packw_layout): chunk i >> 6, sub-chunk
+// (i & 63) / SPL of sw words + 1 pad word each.
+template <int B, int SPL>
+__device__ __forceinline__ uint32_t packw_byte(uint32_t i, uint32_t c, uint32_t cst, uint32_t sw, uint32_t CB) {
+    return (i >> 6) * cst * 4u + ((i & 63u) / (uint32_t)SPL) * (sw + 1u) * 4u + (i & (uint32_t)(SPL - 1)) * CB + c * (uint32_t)B;
+}
+
+// LDS-DMA one frame into the k_packw staging: LDS word k = 64 xi + l of a chunk holds source
+// word k - sub(k), or (pad slot) a dummy; `code` packs sub (2 bits) and the pad flag of every
+// slot xi in 3 bits per lane, computed once per kernel.
+__device__ __forceinline__ void stage_dma_w(const uint8_t *pcm, uint64_t off, uint32_t *stg, uint32_t cw, uint32_t cst,
+                                            uint32_t code, uint32_t wave, uint32_t NW, uint32_t l) {
+    const uint32_t *src = (const uint32_t *)(pcm + off);
+    for (uint32_t ch = wave; ch < 64u; ch += NW) {
+#pragma unroll
+        for (uint32_t xi = 0; xi < 9u; xi++) {
+            const uint32_t cd = (code >> (3u * xi)) & 7u;
+            const uint32_t so = (cd & 4u) ? 0u : 64u * xi + l - cd;
+            if (64u * xi < cst && 64u * xi + l < cst)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + ch * cw + so),
+                                                 (__attribute__((address_space(3))) void *)(stg + ch * cst + 64u * xi), 4,
+                                                 0, 0);
+        }
     }
 }
 
@@ -48,9 +73,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     const uint32_t sfi = wave / WPS, hq = wave % WPS;  // written subframe, part
     const uint32_t C = NC ? (uint32_t)NC : a.channels;
     const uint32_t CB = C * (uint32_t)B;
-    const uint32_t cw = 16u * C * B, cst = cw + stage_pad(C, B);
+    const uint32_t cw = 16u * C * B, cst = packw_cst(C, B, WPS);
+    const uint32_t sw = (uint32_t)SPL * CB / 4u;  // words of one lane's sub-chunk
     const bool dbuf = a.pack_dbuf != 0;
-    const PackLayout LY = pack_layout(C, B, a.image_bytes, dbuf);
+    const PackLayout LY = packw_layout(C, B, WPS, a.image_bytes, dbuf);
+    uint32_t dcode = 0;  // per lane, 3 bits per DMA slot (cst <= 516 words: 9 slots)
+#pragma unroll
+    for (uint32_t xi = 0; xi < 9u; xi++) {
+        const uint32_t k = 64u * xi + l0, sub = k / (sw + 1u), o = k - sub * (sw + 1u);
+        dcode |= (((o == sw || k >= cst) ? 4u : 0u) | (sub & 3u)) << (3u * xi);
+    }
     uint16_t *crct = (uint16_t *)(smem + LY.crc);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
     for (uint32_t i = tid; i < 2048u; i += NT) crct[i] = a.crc_tab[i];
@@ -65,7 +97,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     FrameJob job{}, jn{};
     if (jidx < a.n_jobs) job = a.jobs[jidx];
     if (nxt < a.n_jobs) jn = a.jobs[nxt];
-    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, wave, NW, l0);
+    if (dbuf && jidx < a.n_jobs) stage_dma_w(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, dcode, wave, NW, l0);
     while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);
         if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
@@ -98,12 +130,12 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         if (dbuf) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
-            stage_dma(a.pcm, job.pcm_off, stg, cw, cst, wave, NW, l);
+            stage_dma_w(a.pcm, job.pcm_off, stg, cw, cst, dcode, wave, NW, l);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
-        if (dbuf && nxt < a.n_jobs) stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, wave, NW, l);
+        if (dbuf && nxt < a.n_jobs) stage_dma_w(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, dcode, wave, NW, l);
         FrameJob jnn{};
         if (nn < a.n_jobs) jnn = a.jobs[nn];
         if (skip) {
@@ -119,20 +151,29 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             const uint32_t ia = SPL * l + hq * 64u * SPL;  // == i0, from the opaque lane id
             const uint32_t kind = stereo ? cand : 0u;        // 0 plain channel, 1 R, 2 mid, 3 side
             const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand;
+            // the lane's own samples sit in one sub-chunk: a per-lane base plus immediates
+            const uint32_t lbase = packw_byte<B, SPL>(ia, 0u, cst, sw, CB);
             auto fill = [&](auto KD) {
                 constexpr uint32_t KND = decltype(KD)::value;
-#pragma unroll
-                for (int j = 0; j < KH + SPL; j++) {
-                    const bool before = j < KH && ia + (uint32_t)j < (uint32_t)KH;  // sample index < 0
-                    const uint32_t i = before ? 0u : ia + (uint32_t)j - (uint32_t)KH;
-                    int64_t v;
+                auto get = [&](uint32_t byte) -> int64_t {
                     if constexpr (KND <= 1) {
-                        v = staged_sample<B>(stg, cst, CB, i, chan);
+                        return staged_at<B>(stg, byte + chan * (uint32_t)B);
                     } else {
-                        const int64_t L = staged_sample<B>(stg, cst, CB, i, 0u), R = staged_sample<B>(stg, cst, CB, i, 1u);
-                        v = KND == 2 ? (L + R) >> 1 : L - R;
+                        const int64_t L = staged_at<B>(stg, byte), R = staged_at<B>(stg, byte + (uint32_t)B);
+                        return KND == 2 ? (L + R) >> 1 : L - R;
                     }
+                };
+#pragma unroll
+                for (int j = 0; j < KH; j++) {  // history: the previous sub-chunk / chunk
+                    const bool before = ia + (uint32_t)j < (uint32_t)KH;  // sample index < 0
+                    const uint32_t i = before ? 0u : ia + (uint32_t)j - (uint32_t)KH;
+                    const int64_t v = get(packw_byte<B, SPL>(i, 0u, cst, sw, CB));
                     x[j] = before ? (ST)0 : (ST)v;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < SPL; j++) {
+                    x[KH + j] = (ST)get(lbase + (uint32_t)j * CB);
                     if ((j & 15) == 15) __builtin_amdgcn_sched_barrier(0);
                 }
             };
