@@ -24,3 +24,5 @@ done
 cd $REPO
 python3 tools/pmc_summary.py $OUT $TAG $FRAMES "$CFG:${FRAMES}x${STREAMS}"
 cp $OUT/kt/kt_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
+# profiles/ does not travel back from the GPU box: mirror the summaries under gpurun_out/
+mkdir -p $REPO/gpurun_out/profiles && cp profiles/${TAG}_* $REPO/gpurun_out/profiles/

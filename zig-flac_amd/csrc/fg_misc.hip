@@ -207,6 +207,12 @@ typedef uint32_t md5_v4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FG_MD5_WPE 7
 #endif
 constexpr int kMd5Ahead = FG_MD5_AHEAD;
+// Streams per MD5 workgroup.  The encode kernels fill their SIMDs' register files (k_analyze
+// 4 x 128 VGPRs, k_pack4 8 x 64), so a SIMD that holds an MD5 wave loses one encode wave and its
+// CU one encode workgroup.  Four MD5 waves per workgroup (one per SIMD of one CU) confine that
+// loss to a quarter of the CUs that one-wave workgroups spread it over: C2 step 2.19 -> 2.12 ms
+// (tools/ab_env.sh, FLACGPU_MD5_WG A/B).
+constexpr uint32_t kMd5Wg = 256;
 
 __device__ __forceinline__ void md5_load_block(const uint8_t *p, uint32_t (&m)[16]) {
 #if defined(FG_MD5_DIAG) && FG_MD5_DIAG == 1
@@ -223,7 +229,7 @@ __device__ __forceinline__ void md5_load_block(const uint8_t *p, uint32_t (&m)[1
     }
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FG_MD5_WPE, 8))) k_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens,
+__global__ void __launch_bounds__(kMd5Wg) __attribute__((amdgpu_waves_per_eu(FG_MD5_WPE, 8))) k_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens,
                                                     const uint8_t *final_flags, uint32_t n_streams, Md5State *states,
                                                     uint8_t *digests) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -355,7 +361,7 @@ hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total
 hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *fin,
                               uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_md5_streams, dim3((n + 63) / 64), dim3(64), 0, st, base, offs, lens, fin, n, states,
+    hipLaunchKernelGGL(k_md5_streams, dim3((n + kMd5Wg - 1) / kMd5Wg), dim3(kMd5Wg), 0, st, base, offs, lens, fin, n, states,
                        digests);
     return hipGetLastError();
 }
