@@ -406,10 +406,16 @@ static void calc_residuals(const int64_t *s, uint32_t n, unsigned k, int wide, i
 /*  6. residual e(i) = x(i) - ((sum_t c_t x(i-1-t)) >> shift) in i64; an   */
 /*     order with a coded residual outside [-2^30, 2^30) is unusable (its  */
 /*     zigzag code then fits 31 bits, so an escape is always possible);    */
-/*  7. every order 1..Q (Q < n) gets the fixed path's Rice search with q   */
-/*     warm-ups; subframe total = rice + q (bps' + 15) + 9; the lowest      */
-/*     order with the strictly smallest total wins, and it replaces the     */
-/*     fixed/verbatim choice only if strictly smaller (totals incl. warm-ups)*/
+/*  7. order selection by the Levinson-Durbin error (as libFLAC without    */
+/*     its exhaustive search): among orders 1..Q (Q < n) whose coefficients */
+/*     quantise, the lowest q with the smallest                             */
+/*       key(q) = l2(err_q) * (n / 2) + q (bps' + 15)   (IEEE double, this  */
+/*     operation order; err_q = the LD error after order q; l2(x) = (e-1) + */
+/*     (2f-1) for x = f 2^e, f in [0.5,1): a piecewise-linear log2 made of  */
+/*     exact IEEE operations; err_q <= 0 -> key = -1e300);                  */
+/*  8. that one order gets the fixed path's Rice search with q warm-ups;    */
+/*     subframe total = rice + q (bps' + 15) + 9; it replaces the fixed/    */
+/*     verbatim choice only if strictly smaller (totals incl. warm-ups)     */
 /* ===================================================================== */
 #define LPC_XW_BITS 25u
 
@@ -436,7 +442,8 @@ int oracle_lpc_autocorr(const int64_t *x, uint32_t n, unsigned max_lag, int64_t 
     return sh;
 }
 
-int oracle_lpc_levinson(const int64_t *R, unsigned max_order, double *coefs) {
+/* Levinson-Durbin; errs[m] (if non-NULL) = the prediction error after order m + 1 */
+int oracle_lpc_levinson_err(const int64_t *R, unsigned max_order, double *coefs, double *errs) {
     double r[ORACLE_LPC_MAX_ORDER + 1], a[ORACLE_LPC_MAX_ORDER], tmp[ORACLE_LPC_MAX_ORDER];
     for (unsigned i = 0; i <= max_order; i++) r[i] = (double)R[i];
     if (!(r[0] > 0.0)) return 0;
@@ -459,9 +466,23 @@ int oracle_lpc_levinson(const int64_t *R, unsigned max_order, double *coefs) {
         valid = m + 1;
         double kk = k * k;
         err = err * (1.0 - kk);
+        if (errs) errs[m] = err;
         if (!(err > 0.0)) break;
     }
     return (int)valid;
+}
+
+int oracle_lpc_levinson(const int64_t *R, unsigned max_order, double *coefs) {
+    return oracle_lpc_levinson_err(R, max_order, coefs, NULL);
+}
+
+/* order-selection key of contract step 7 */
+double oracle_lpc_order_key(double err, unsigned q, uint32_t n, unsigned bps) {
+    if (!(err > 0.0)) return -1e300;
+    int e;
+    const double f = frexp(err, &e);
+    const double l2 = (double)(e - 1) + (2.0 * f - 1.0);
+    return l2 * (0.5 * (double)n) + (double)(q * (bps + ORACLE_LPC_PRECISION));
 }
 
 int oracle_lpc_quantize(const double *a, unsigned order, unsigned precision, int32_t *q, int *shift) {
@@ -533,13 +554,32 @@ static void lpc_search(sub_t *sub, const int64_t *s, uint32_t n, const oracle_co
         if (s[i] != (int64_t)(int32_t)s[i]) return; /* 33-bit side: no LPC (contract step 0) */
     int64_t R[ORACLE_LPC_MAX_ORDER + 1];
     static __thread double coefs[ORACLE_LPC_MAX_ORDER * ORACLE_LPC_MAX_ORDER];
+    double errs[ORACLE_LPC_MAX_ORDER];
     oracle_lpc_autocorr(s, n, Q, R);
-    int valid = oracle_lpc_levinson(R, Q, coefs);
-    int32_t *e = (int32_t *)malloc(n * sizeof(int32_t));
+    int valid = oracle_lpc_levinson_err(R, Q, coefs, errs);
+    /* step 7: the order with the smallest key (lowest q on ties) among those that quantise */
+    unsigned qs = 0;
+    double best_key = 0.0;
+    int32_t cs[ORACLE_LPC_MAX_ORDER];
+    int shs = 0;
     for (unsigned q = 1; q <= (unsigned)valid; q++) {
         int32_t c[ORACLE_LPC_MAX_ORDER];
         int shift;
         if (oracle_lpc_quantize(coefs + (q - 1) * ORACLE_LPC_MAX_ORDER, q, ORACLE_LPC_PRECISION, c, &shift)) continue;
+        const double key = oracle_lpc_order_key(errs[q - 1], q, n, bps);
+        if (qs == 0 || key < best_key) {
+            qs = q;
+            best_key = key;
+            memcpy(cs, c, q * sizeof(int32_t));
+            shs = shift;
+        }
+    }
+    if (qs == 0) return;
+    int32_t *e = (int32_t *)malloc(n * sizeof(int32_t));
+    /* step 8: the selected order only */
+    for (unsigned q = qs; q == qs; q++) {
+        const int32_t *c = cs;
+        const int shift = shs;
         if (lpc_residuals(s, n, q, c, shift, e)) continue;
         rice_cfg rc;
         memset(&rc, 0, sizeof(rc));

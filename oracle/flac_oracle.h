@@ -145,6 +145,8 @@ size_t oracle_max_frame_bytes(uint32_t block_size, uint32_t bit_depth, uint32_t 
  * quantize: returns 0 and the shift, or -1 if the order is not representable. */
 int oracle_lpc_autocorr(const int64_t *x, uint32_t n, unsigned max_lag, int64_t *R);
 int oracle_lpc_levinson(const int64_t *R, unsigned max_order, double *coefs);
+int oracle_lpc_levinson_err(const int64_t *R, unsigned max_order, double *coefs, double *errs);
+double oracle_lpc_order_key(double err, unsigned q, uint32_t n, unsigned bps);
 int oracle_lpc_quantize(const double *a, unsigned order, unsigned precision, int32_t *q, int *shift);
 
 /* Exposed pieces for unit tests. */

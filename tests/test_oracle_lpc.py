@@ -173,3 +173,71 @@ def test_prediction_zero_is_the_reference_path():
     a, _, _ = oracle_ref.encode_stream(pcm, 2, 16, 44100)
     b, _, _ = oracle_ref.encode_stream(pcm, 2, 16, 44100, lpc=0)
     assert a == b
+
+
+def _py_levinson_err(R, Q):
+    r = [float(v) for v in R]
+    errs = []
+    if not r[0] > 0.0:
+        return errs
+    err, a = r[0], []
+    for m in range(Q):
+        acc = r[m + 1]
+        for t in range(m):
+            acc = acc - a[t] * r[m - t]
+        k = acc / err
+        a = [a[t] - k * a[m - 1 - t] for t in range(m)] + [k]
+        err = err * (1.0 - k * k)
+        errs.append(err)
+        if not err > 0.0:
+            break
+    return errs
+
+
+def _py_key(err, q, n, bps):
+    # contract step 7: l2(x) = (e - 1) + (2f - 1) for x = f 2^e, f in [0.5, 1)
+    if not err > 0.0:
+        return -1e300
+    f, e = math.frexp(err)
+    l2 = float(e - 1) + (2.0 * f - 1.0)
+    return l2 * (0.5 * float(n)) + float(q * (bps + 15))
+
+
+def test_levinson_errors_and_order_key_match_python():
+    L = _lib()
+    L.oracle_lpc_levinson_err.restype = ctypes.c_int
+    L.oracle_lpc_order_key.restype = ctypes.c_double
+    L.oracle_lpc_order_key.argtypes = [ctypes.c_double, ctypes.c_uint, ctypes.c_uint32, ctypes.c_uint]
+    for stream in range(6):
+        x = synth.synth_samples(4096, 1, 24, 96000, stream=stream)[:, 0].astype(np.int64)
+        _, R = _autocorr(x, 12)
+        Ra = (ctypes.c_int64 * 13)(*R)
+        C = (ctypes.c_double * (32 * 32))()
+        E = (ctypes.c_double * 32)()
+        valid = L.oracle_lpc_levinson_err(Ra, 12, C, E)
+        ref = _py_levinson_err(R, 12)
+        assert valid == len(ref) and list(E)[:valid] == ref  # bit-identical doubles
+        for q in range(1, valid + 1):
+            for n, bps in [(4096, 24), (1000, 17), (13, 32)]:
+                assert L.oracle_lpc_order_key(ref[q - 1], q, n, bps) == _py_key(ref[q - 1], q, n, bps)
+    assert L.oracle_lpc_order_key(0.0, 3, 4096, 16) == -1e300
+    # the piecewise-linear log2 is exact at powers of two: key(2^10) = 10 n/2 + q (bps + 15)
+    assert L.oracle_lpc_order_key(1024.0, 2, 4096, 16) == 10 * 2048 + 2 * 31
+
+
+def test_lpc_selects_the_order_of_the_smallest_key():
+    # the written LPC subframe of a predictable signal carries the key-selected order
+    n = 4096
+    t = np.arange(n)
+    x = (2 ** 20 * np.sin(t * 1.3) + 2 ** 19 * np.sin(t * 2.1) + 3 * np.sin(t * 0.37)).astype(np.int64)
+    planes = [np.ascontiguousarray(x).astype(np.int32)]
+    _, rec = oracle_ref.encode_frame(planes, n, 0, 1, 24, 48000, lpc=8)
+    sub = rec.written[0]
+    assert sub.type == 3
+    _, R = _py_autocorr(x, 8)
+    errs = _py_levinson_err(R, 8)
+    coefs = _py_levinson(R, 8)
+    bps = 24 - sub.waste
+    keys = [(_py_key(errs[q - 1], q, n, bps), q) for q in range(1, len(errs) + 1)
+            if _py_quantize(coefs[q - 1]) is not None]
+    assert sub.order == min(keys)[1]

@@ -855,13 +855,16 @@ __device__ __forceinline__ void lpc_autocorr(const ST (&s)[64], uint32_t n, uint
 
 // Levinson-Durbin + quantisation of every order 1..Q: tab[(q-1)*13 + t] = coefficient t of
 // order q (0 past q), tab[(q-1)*13 + 12] = its shift, or -1 if the order is unusable.  The
-// recursion is serial and runs on every lane; lane m keeps the coefficients of order m+1 as
-// they are produced and quantises them itself afterwards (each order's error-feedback chain
-// is independent), so the quantisation costs one order's chain, not all of them in series.
+// recursion is serial and runs on every lane; lane m keeps the coefficients of order m+1 and
+// the LD error after it as they are produced and quantises them itself afterwards (each
+// order's error-feedback chain is independent), so the quantisation costs one order's chain,
+// not all of them in series.  Returns the selected order (contract step 7: the lowest q with
+// the smallest key l2(err_q) * n/2 + q (bps' + 15) among the orders that quantise), 0 if none.
 template <int W>
-__device__ __forceinline__ void lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q, int32_t *tab, uint32_t lane) {
+__device__ __forceinline__ uint32_t lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q, int32_t *tab, uint32_t lane,
+                                              uint32_t n, uint32_t bps) {
 #pragma clang fp contract(off)
-    double r[W + 1], a[W], tmp[W], mine[W];
+    double r[W + 1], a[W], tmp[W], mine[W], myerr = 0.0;
 #pragma unroll
     for (int i = 0; i <= W; i++) r[i] = (double)R[i];
 #pragma unroll
@@ -895,6 +898,7 @@ __device__ __forceinline__ void lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q,
             for (int t = 0; t <= m; t++) mine[t] = me ? a[t] : mine[t];
             const double kk = k * k;
             err = err * (1.0 - kk);
+            myerr = me ? err : myerr;
             live = err > 0.0;
         }
     }
@@ -939,6 +943,29 @@ __device__ __forceinline__ void lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q,
         for (int t = 0; t < kLpcMax; t++) tab[m * 13u + t] = (t < W) ? qc[t < W ? t : 0] : 0;
         tab[m * 13u + 12u] = shq;
     }
+    // selection key of order lane + 1 (oracle_lpc_order_key), as an integer with the same order
+    double key = -1e300;
+    if (myerr > 0.0) {
+        int e;
+        const double f = frexp(myerr, &e);
+        const double l2 = (double)(e - 1) + (2.0 * f - 1.0);
+        key = l2 * (0.5 * (double)n) + (double)((lane + 1u) * (bps + (uint32_t)kLpcPrec));
+    }
+    const int64_t kb = __builtin_bit_cast(int64_t, key);
+    const uint64_t ko = (uint64_t)(kb < 0 ? ~kb : (kb | INT64_MIN));  // monotone in key
+    const bool ok = have && shq >= 0 && lane < Q;
+    uint32_t qsel = 0;
+    uint64_t kbest = 0;
+#pragma unroll
+    for (int t = 0; t < W; t++) {  // ascending order, strict "<": the lowest order wins ties
+        const uint32_t okt = (uint32_t)__builtin_amdgcn_readlane((int)ok, t);
+        const uint64_t kt = rdl64(ko, t);
+        if (okt && (qsel == 0 || kt < kbest)) {
+            qsel = (uint32_t)t + 1u;
+            kbest = kt;
+        }
+    }
+    return qsel;
 }
 
 // Prediction sum_t c[t] * x[j-1-t] over the lane's samples and the previous lane's
@@ -1595,6 +1622,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             const uint32_t Q = a.lpc_order;
             if (lpc_on && R.type != 0 && n > Q) {
                 bool fits;
+                uint32_t qsel = 0;  // the order selected by its LD error (contract step 7)
                 {
                     int32_t x[64];
                     fits = __all(load_lpc_samples<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, R.waste, x));
@@ -1602,7 +1630,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                         int64_t Rac[LPW + 1];
                         lpc_autocorr<LPW, int32_t>(x, n, l, Rac);
                         __builtin_amdgcn_sched_barrier(0);
-                        lpc_coefs<LPW>(Rac, Q, ltab, l);
+                        qsel = lpc_coefs<LPW>(Rac, Q, ltab, l, n, bps);
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1621,7 +1649,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                         for (int j = 0; j < 64; j++) xm = max(xm, (uint32_t)(x[j] < 0 ? -(int64_t)x[j] : x[j]));
                         xmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max32(xm));
                     }
-                    for (uint32_t q = 1; q <= Q; q++) {
+                    // contract step 8: the selected order only (`continue` ends the search)
+                    for (uint32_t q = qsel; q != 0; q = 0) {
                         const int32_t shq = __builtin_amdgcn_readfirstlane(ltab[(q - 1u) * 13u + 12u]);
                         if (shq < 0) continue;
                         int32_t c[LPW];

@@ -212,7 +212,7 @@ constexpr int kMd5Ahead = FG_MD5_AHEAD;
 // CU one encode workgroup.  Four MD5 waves per workgroup (one per SIMD of one CU) confine that
 // loss to a quarter of the CUs that one-wave workgroups spread it over: C2 step 2.19 -> 2.12 ms
 // (tools/ab_env.sh, FLACGPU_MD5_WG A/B).
-constexpr uint32_t kMd5Wg = 256;
+constexpr uint32_t kMd5Wg = kMd5StreamsPerWg;
 
 __device__ __forceinline__ void md5_load_block(const uint8_t *p, uint32_t (&m)[16]) {
 #if defined(FG_MD5_DIAG) && FG_MD5_DIAG == 1
