@@ -38,7 +38,13 @@ torch.cuda.synchronize()
 print("encode ms/launch", enc.kernel_time(0))
 L.flacgpu_debug_stamps(enc.ctx, out, 0)
 WA = 4 if CH == 2 else CH                        # analysis waves per frame (stereo: L, R, M, S)
-WP = 8 if (CH == 2 and BITS == 16) else CH       # pack waves per frame (k_pack4: 4 per written subframe)
+NOUT = 2 if CH == 2 else CH
+if CH == 2 and BITS == 16 and LPC == 0:
+    WP = 8                                         # k_pack4: 4 waves per written subframe
+elif BITS == 32 or NOUT > 2:
+    WP = NOUT * (4 if NOUT <= 4 else 2)            # k_packw: WPS waves per written subframe
+else:
+    WP = NOUT                                      # k_pack: one wave per written subframe
 for base, names, label in [(0, NAMES, "analysis"), (16, PNAMES, "pack")]:
     tot = sum(out[base:base + len(names)])
     print(f"-- {label}")
