@@ -2109,7 +2109,21 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
                 int32_t c[LPW];
 #pragma unroll
                 for (int t = 0; t < LPW; t++) c[t] = (t < kLpcMax) ? __builtin_amdgcn_readfirstlane((int32_t)sd->coef[t < kLpcMax ? t : 0]) : 0;
-                residuals_lpc_inplace<LPW, ST>(s, hs, c, (uint32_t)(int32_t)sd->lpc_shift, k, l);
+                // taps bucketed by order (c[t] = 0 past it), as in the analysis kernel
+                auto lpc = [&](auto WT) {
+                    constexpr int W = decltype(WT)::value;
+                    ST hsw[W];
+                    int32_t cw[W];
+#pragma unroll
+                    for (int t = 0; t < W; t++) {
+                        hsw[t] = hs[t];
+                        cw[t] = c[t];
+                    }
+                    residuals_lpc_inplace<W, ST>(s, hsw, cw, (uint32_t)(int32_t)sd->lpc_shift, k, l);
+                };
+                if (k <= 4u) lpc(ic<4>{});
+                else if (LPW <= 8 || k <= 8u) lpc(ic<(LPW < 8 ? LPW : 8)>{});
+                else lpc(ic<LPW>{});
             }
         }
 

@@ -98,6 +98,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     if (jidx < a.n_jobs) job = a.jobs[jidx];
     if (nxt < a.n_jobs) jn = a.jobs[nxt];
     if (dbuf && jidx < a.n_jobs) stage_dma_w(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, dcode, wave, NW, l0);
+#ifdef FG_STAMPS
+    uint64_t ph_[16] = {};
+    uint64_t tprev_ = __builtin_amdgcn_s_memtime();
+#endif
     while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);
         if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
@@ -127,13 +131,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         for (uint32_t t = 0; t < sfi; t++) sub_start += sd0[t].bits;
 
         // ---- 1. PCM (double-buffered: DMA'd during the previous frame) -> samples
+        STAMP(7);
         if (dbuf) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             stage_dma_w(a.pcm, job.pcm_off, stg, cw, cst, dcode, wave, NW, l);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        STAMP(8);
         __syncthreads();
+        STAMP(0);
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         if (dbuf && nxt < a.n_jobs) stage_dma_w(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, dcode, wave, NW, l);
         FrameJob jnn{};
@@ -181,12 +188,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             else if (kind == 2) fill(ic<2>{});
             else fill(ic<3>{});
         }
+        STAMP(9);
         // lane offsets: the part's base = the analysis kernel's segment lengths before it
         const uint32_t lbs = wave_incl_scan32(lb);
         const uint32_t qbase = hq ? rdl(lbs, (int)(SPL * hq - 1u)) : 0u;
+        STAMP(10);
         bar_lds();  // staging dead: zero the image
+        STAMP(1);
         const uint32_t Wz = (fbytes + 3u) / 4u + 2u;
         for (uint32_t i = tid; i < Wz; i += NT) img[i] = 0;
+        STAMP(2);
 
         // ---- 2. waste shift and residuals, lengths of this lane's codes
         const uint32_t bps = bd - w;
@@ -217,13 +228,21 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
 #pragma unroll
                 for (int t = 0; t < LPW; t++) c[t] = __builtin_amdgcn_readfirstlane((int32_t)sd->coef[t < kLpcMax ? t : 0]);
                 const uint32_t shift = (uint32_t)(int32_t)sd->lpc_shift;
+                // LPC runs on i32 samples only (contract step 0), so every product is a
+                // v_mad_i64_i32 even for 32-bit input; taps bucketed by order (c[t] = 0 past it)
+                auto lpc = [&](auto WT) {
+                    constexpr int W = decltype(WT)::value;
 #pragma unroll
-                for (int j = 0; j < SPL; j++) {
-                    int64_t acc = 0;
+                    for (int j = 0; j < SPL; j++) {
+                        int64_t acc = 0;
 #pragma unroll
-                    for (int t = 0; t < LPW; t++) acc += (int64_t)c[t] * (int64_t)x[KH + j - 1 - t];
-                    r[j] = (uint32_t)(int32_t)((int64_t)x[KH + j] - (acc >> shift));
-                }
+                        for (int t = 0; t < W; t++) acc += (int64_t)c[t] * (int64_t)(int32_t)x[KH + j - 1 - t];
+                        r[j] = (uint32_t)((int32_t)x[KH + j] - (int32_t)(acc >> shift));
+                    }
+                };
+                if (k <= 4u) lpc(ic<4>{});
+                else if (LPW <= 8 || k <= 8u) lpc(ic<(LPW < 8 ? LPW : 8)>{});
+                else lpc(ic<LPW>{});
             }
         } else {
 #pragma unroll
@@ -266,6 +285,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         }
         const uint32_t lane_off = wave_incl_scan32(len) - len;
         bar_lds();  // image zeroed
+        STAMP(3);
         if (tid < 4) {
             const uint32_t hv = F->hdr[tid];
             if (hv) atomicOr(&img[tid], hv);
@@ -359,6 +379,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             }
         }
         bar_lds();
+        STAMP(4);
 
         // ---- 4. CRC-16 of the frame (one chain of 2H words per thread, see k_pack4)
         {
@@ -381,11 +402,17 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             put_bits(img, Lb * 8u, crc, 16);
         }
         bar_lds();
+        STAMP(5);
 
         // ---- 5. image -> out[D, D + fbytes)
         store_frame16(img, a.out, D, fbytes, tid, NT);
         // single buffer: the next frame's staging overwrites the image
         if (!dbuf) __syncthreads();
+        STAMP(6);
         jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
     }  // persistent frame loop
+#ifdef FG_STAMPS
+    if (l0 == 0 && a.stamps)
+        for (int i = 0; i < 11; i++) atomicAdd(&a.stamps[16 + i], (unsigned long long)ph_[i]);
+#endif
 }
