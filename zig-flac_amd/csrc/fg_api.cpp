@@ -407,7 +407,10 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     c->image_bytes = fg_round16(frame_bound_bytes(kBlock, c->C, c->bits, c->stereo != 0) + 16u);
     c->desc_stride = desc_stride(n_out);
     const bool lpc = c->cfg.prediction != 0;
-    c->stage_dbuf = ana_layout(c->C, c->B, nw, true, true, lpc).total <= 160u * 1024u;
+    // 24-bit LPC analysis runs three waves per SIMD (fg_device.hpp): double-buffer only where
+    // three workgroups still fit the LDS
+    const uint32_t ana_wgs = (lpc && c->B == 3) ? 3u : 1u;
+    c->stage_dbuf = ana_layout(c->C, c->B, nw, true, true, lpc).total * ana_wgs <= 160u * 1024u;
     c->lds = ana_layout(c->C, c->B, nw, true, c->stage_dbuf, lpc).total;
     c->lds_tail = ana_layout(c->C, c->B, nw, false, false, lpc).total;
     // pack: double-buffer the staging when that keeps the register-limited occupancy

@@ -1066,12 +1066,17 @@ __device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int3
 #ifndef FG_PACK_MINW
 #define FG_PACK_MINW 4
 #endif
+
 template <int B, int CLS, bool FULL, int MAXT, int NC, int LPW>
 // i64 samples (32-bit input), the tail kernels' LDS tables and the LPC search need
 // the larger register budget (2 waves/SIMD); the rest fits 128 VGPRs (4 waves/SIMD).
 //   LPW  : 0 = fixed prediction only (the reference); 8 / 12 = LPC taps held in
 //          registers (orders up to LPW, build-defined extension)
-__global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LPW == 0) ? FG_MINW : 2))
+// 24-bit LPC full frames: three waves per SIMD (168 VGPRs, more scratch, single-buffered staging
+// so three workgroups fit the LDS) beat two with double buffering: c3 analysis 5.56 -> 4.80 ms
+// (the 32-bit variant spills too much at 168: c5 8.7 -> 10.7 ms, so it stays at two).
+__global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LPW == 0) ? FG_MINW
+                                          : ((FULL && LPW > 0 && CLS == 24) ? 3 : 2)))
     k_analyze(EncodeArgs a) {
     using ST = typename Cls<CLS>::S;
     // LPC residuals may reach 2^30 in magnitude: 16-sample sums need 64 bits
