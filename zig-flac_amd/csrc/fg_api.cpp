@@ -23,7 +23,8 @@ namespace fg {
 hipError_t launch_stage(int stage, const EncodeArgs &a, bool full, uint32_t threads, uint32_t lds, hipStream_t st);
 hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, uint32_t stride, uint64_t first,
                             uint32_t n_frames, hipStream_t st);
-hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, hipStream_t st);
+hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, uint64_t *part,
+                       hipStream_t st);
 hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *fin,
                               uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st);
 hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipStream_t st);
@@ -93,6 +94,8 @@ struct flacgpu_ctx {
     FrameRec *d_records = nullptr;
     unsigned long long *d_stamps = nullptr;
     bool records_on = false;
+    uint64_t *d_scan_part = nullptr;  // per-4096-frame block sums of the multi-workgroup scan
+    uint32_t scan_part_cap = 0;
     std::vector<FrameRec> h_records;
     bool timing = false;
     std::vector<TimedLaunch> pending;
@@ -255,7 +258,16 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     }
     {
         Timed t(c, FLACGPU_K_SCAN, st);
-        HIPCHK(launch_scan(d_fbytes, d_offsets, d_total, (uint32_t)n_frames, st));
+        // multi-workgroup scan: per-block sums in a grow-only context buffer
+        const uint32_t nb = (uint32_t)((n_frames + 4095u) / 4096u);
+        if (nb > c->scan_part_cap) {
+            hipFree(c->d_scan_part);
+            c->d_scan_part = nullptr;
+            c->scan_part_cap = 0;
+            HIPCHK(hipMalloc(&c->d_scan_part, (size_t)nb * 8u));
+            c->scan_part_cap = nb;
+        }
+        HIPCHK(launch_scan(d_fbytes, d_offsets, d_total, (uint32_t)n_frames, c->d_scan_part, st));
     }
     {
         Timed t(c, FLACGPU_K_PACK, st);
@@ -511,6 +523,7 @@ void flacgpu_close(flacgpu_ctx *c) {
     hipFree(c->d_crc_pow);
     hipFree(c->d_crc_pow4);
     hipFree(c->d_crc_join);
+    hipFree(c->d_scan_part);
     hipFree(c->d_err);
     hipFree(c->d_ctr);
     hipFree(c->d_jobs);

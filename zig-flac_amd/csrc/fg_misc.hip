@@ -125,6 +125,89 @@ __global__ void __launch_bounds__(1024) k_scan(const uint32_t *sizes, uint64_t *
 }
 
 // ------------------------------------------------------------------------
+// The same scan over many workgroups (k_scan, one workgroup, took ~60 us for 65536 frames:
+// one CU's memory latency): block b = frames [4096 b, 4096 b + 4096), four per thread.
+// k_scan_part writes each block's sum; k_scan_blocks adds the sums of the blocks before
+// its own to its workgroup's exclusive scan.
+// ------------------------------------------------------------------------
+constexpr uint32_t kScanBlock = 4096;
+
+__device__ __forceinline__ void scan_load4(const uint32_t *sizes, uint32_t i0, uint32_t n, bool vec, uint32_t (&v)[4]) {
+    if (vec && i0 + 4u <= n) {
+        const uint4 q = *(const uint4 *)(sizes + i0);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = (i0 + (uint32_t)k < n) ? sizes[i0 + k] : 0u;
+    }
+}
+
+// workgroup exclusive scan of one u64 per thread (1024 threads); *blk = the workgroup total
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t acc, uint64_t *wsum, uint64_t *blk) {
+    const uint32_t t = threadIdx.x, l = lane_id_m(), w = t >> 6;
+    uint64_t x = acc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d);
+        if (l >= (uint32_t)d) x += y;
+    }
+    if (l == 63) wsum[w] = x;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) {
+        const uint64_t v = wsum[i];
+        pre += i < w ? v : 0u;
+        tot += v;
+    }
+    *blk = tot;
+    return pre + x - acc;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_part(const uint32_t *sizes, uint64_t *part, uint32_t n) {
+    __shared__ uint64_t wsum[16];
+    const bool vec = (reinterpret_cast<uintptr_t>(sizes) & 15u) == 0;
+    uint32_t v[4];
+    scan_load4(sizes, blockIdx.x * kScanBlock + 4u * threadIdx.x, n, vec, v);
+    uint64_t blk;
+    (void)block_excl_scan((uint64_t)v[0] + v[1] + v[2] + v[3], wsum, &blk);
+    if (threadIdx.x == 0) part[blockIdx.x] = blk;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_blocks(const uint32_t *sizes, uint64_t *offsets, uint64_t *total,
+                                                      const uint64_t *part, uint32_t n) {
+    __shared__ uint64_t wsum[16], bsum[16];
+    const uint32_t t = threadIdx.x, b = blockIdx.x;
+    // sum of the blocks before this one
+    uint64_t p = 0;
+    for (uint32_t j = t; j < b; j += 1024u) p += part[j];
+    uint64_t before;
+    (void)block_excl_scan(p, bsum, &before);
+    const uint32_t i0 = b * kScanBlock + 4u * t;
+    const bool vec = ((reinterpret_cast<uintptr_t>(sizes) | reinterpret_cast<uintptr_t>(offsets)) & 15u) == 0;
+    uint32_t v[4];
+    scan_load4(sizes, i0, n, vec, v);
+    uint64_t blk;
+    uint64_t run = before + block_excl_scan((uint64_t)v[0] + v[1] + v[2] + v[3], wsum, &blk);
+    uint64_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        o[k] = run;
+        run += v[k];
+    }
+    if (vec && i0 + 4u <= n) {
+        ulonglong2 *o2 = (ulonglong2 *)(offsets + i0);
+        o2[0] = make_ulonglong2(o[0], o[1]);
+        o2[1] = make_ulonglong2(o[2], o[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (i0 + (uint32_t)k < n) offsets[i0 + k] = o[k];
+    }
+    if (b == gridDim.x - 1u && t == 0) *total = before + blk;
+}
+
+// ------------------------------------------------------------------------
 // MD5 (md5.zig / RFC 1321): one lane per independent stream
 // ------------------------------------------------------------------------
 constexpr uint32_t kMd5K[64] = {
@@ -353,8 +436,16 @@ hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipSt
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, hipStream_t st) {
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, sizes, offsets, total, n);
+// part: ceil(n / 4096) u64 of scratch (NULL: the one-workgroup k_scan)
+hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, uint64_t *part,
+                       hipStream_t st) {
+    if (!part) {
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, sizes, offsets, total, n);
+        return hipGetLastError();
+    }
+    const uint32_t nb = (n + kScanBlock - 1u) / kScanBlock;
+    if (nb > 1u) hipLaunchKernelGGL(k_scan_part, dim3(nb), dim3(1024), 0, st, sizes, part, n);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, sizes, offsets, total, part, n);
     return hipGetLastError();
 }
 
