@@ -236,3 +236,36 @@ def test_sync_check_reports_output_too_small():
         res, _ = _run_plan(enc, pcm + bytes(64), [0], lengths)
         ref, _, _ = oracle_ref.encode_stream(pcm, ch, bits, rate)
         assert res[0][0] == ref
+
+
+@pytest.mark.parametrize("misalign", [False, True])
+def test_plan_scan_spans_blocks(misalign):
+    # > 2 x 4096 frames (block size 16): the multi-workgroup scan's block sums; the size and
+    # offset arrays optionally at 4- / 8-byte (not 16-byte) alignment, its element-wise path
+    torch, dev = _torch()
+    ch, bits, rate, bs = 2, 16, 44100, 16
+    n = 16 * 9000 + 5
+    pcm = synth.synth_pcm(n, ch, bits, rate, stream=3)
+    with _encoder(ch, bits, rate, max_frames=64, block_size=bs) as enc:
+        plan = enc.plan([0], [n])
+        nf = int(plan.n_frames)
+        assert nf == 9001
+        d_pcm = torch.from_numpy(np.frombuffer(pcm, dtype=np.uint8).copy()).to(dev)
+        d_out = torch.zeros(int(plan.out_bound), dtype=torch.uint8, device=dev)
+        fb_buf = torch.zeros(nf + 4, dtype=torch.int32, device=dev)
+        off_buf = torch.zeros(nf + 2, dtype=torch.int64, device=dev)
+        d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
+        sh_fb, sh_off = (1, 1) if misalign else (0, 0)
+        st = torch.cuda.current_stream(dev)
+        enc.encode_plan_device(plan, d_pcm.data_ptr(), d_out.data_ptr(), int(plan.out_bound),
+                               fb_buf.data_ptr() + 4 * sh_fb, off_buf.data_ptr() + 8 * sh_off, d_tot.data_ptr(), None,
+                               st.cuda_stream)
+        enc.sync_check(st.cuda_stream)
+        plan.close()
+        sizes = fb_buf[sh_fb:sh_fb + nf].cpu().numpy().astype(np.int64)
+        offs = off_buf[sh_off:sh_off + nf].cpu().numpy()
+        total = int(d_tot[0].item())
+    assert offs[0] == 0 and (np.diff(offs) == sizes[:-1]).all() and total == int(sizes.sum())
+    ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, ch, bits, rate, block=bs)
+    assert [int(x) for x in sizes] == ref_sizes
+    assert d_out[:total].cpu().numpy().tobytes() == ref
