@@ -130,6 +130,8 @@ struct EncodeArgs {
     uint32_t crc_hmax4;
     FrameRec *records;          // optional decision records [slot]
     unsigned long long *stamps; // diagnostic builds (-DFG_STAMPS): per-phase clock sums
+    uint32_t ch_split;          // full-frame analysis: 1 = one workgroup per channel half (channels
+                                // = the half's count), frame totals by k_frame_totals
 };
 
 }  // namespace fg

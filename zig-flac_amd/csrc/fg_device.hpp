@@ -491,14 +491,30 @@ struct CandRes {
 // (fg_layout.hpp): 16 instructions of 1 KiB, lane i of instruction k filling byte 16i of
 // block k from 16-B group i >> 2 of chunk 4k + (i & 3).  Padded layouts: each
 // wave-instruction moves <= 64 dwords of one 64-sample chunk (M0 = that chunk's base).
+// drh != 0: channel half `half` only -- the staged chunk holds drh of every 2 drh source dwords
+// of each interchannel row (cw = the half row's dwords x 64), see k_analyze's split mode.
 __device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint32_t *stg, uint32_t cw, uint32_t cst,
-                                          uint32_t wave, uint32_t NW, uint32_t l, bool ilv = false) {
+                                          uint32_t wave, uint32_t NW, uint32_t l, bool ilv = false, uint32_t drh = 0,
+                                          uint32_t half = 0) {
     const uint32_t *src = (const uint32_t *)(pcm + off);
     if (ilv) {
         for (uint32_t k = wave; k < 16u; k += NW)
             __builtin_amdgcn_global_load_lds(
                 (__attribute__((address_space(1))) void *)(src + (4u * k + (l & 3u)) * 64u + 4u * (l >> 2)),
                 (__attribute__((address_space(3))) void *)(stg + 272u * k), 16, 0, 0);
+        return;
+    }
+    if (drh) {
+        const float inv = 1.0f / (float)drh;  // x / drh exactly for x < 2^10, drh <= 4
+        for (uint32_t ch = wave; ch < 64u; ch += NW) {
+            for (uint32_t x0 = 0; x0 < cw; x0 += 64u) {
+                const uint32_t x = x0 + l, r = (uint32_t)((float)x * inv), k = x - r * drh;
+                if (x < cw)
+                    __builtin_amdgcn_global_load_lds(
+                        (__attribute__((address_space(1))) void *)(src + ch * 2u * cw + r * 2u * drh + half * drh + k),
+                        (__attribute__((address_space(3))) void *)(stg + ch * cst + x0), 4, 0, 0);
+            }
+        }
         return;
     }
     for (uint32_t ch = wave; ch < 64u; ch += NW) {
@@ -1112,14 +1128,23 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     if (blockIdx.x == 0 && tid == 0) a.work_ctr[2] = a.work_ctr[3] = 0u;  // the pack kernel's queues
     if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
     __syncthreads();
+    // Channel halves (a.ch_split, full frames of 4+ independent channels staged single-buffered):
+    // a work item is (frame, half); the half's C channels are dwords [half drh, half drh + drh)
+    // of every 2 drh-dword interchannel row, so two or three workgroups share a CU where one
+    // whole 96-KiB frame would fill its LDS.  The frame-level fields are completed by
+    // k_frame_totals after the launch.
+    const uint32_t ssh = (FULL && a.ch_split) ? 1u : 0u;
+    const uint32_t drh = ssh ? C * (uint32_t)B / 4u : 0u;
+    const uint32_t n_items = a.n_jobs << ssh;
     uint32_t jidx = blockIdx.x, buf = 0;
     uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
     FrameJob job{}, jn{};
-    if (jidx < a.n_jobs) job = a.jobs[jidx];
-    if (nxt < a.n_jobs) jn = a.jobs[nxt];
-    if (dbuf && jidx < a.n_jobs) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0, NC == 2 && B == 2);
-    while (jidx < a.n_jobs) {
+    if (jidx < n_items) job = a.jobs[jidx >> ssh];
+    if (nxt < n_items) jn = a.jobs[nxt >> ssh];
+    if (dbuf && jidx < n_items) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0, NC == 2 && B == 2, drh, jidx & ssh);
+    while (jidx < n_items) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
+        const uint32_t half = jidx & ssh;
         STAMP(8);
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.stage1 : LY.stage0));
@@ -1130,7 +1155,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         } else if constexpr (FULL) {
             // one buffer (the frame is too large for two): every wave issues all its LDS-DMA
             // loads at once and waits once -- not one load-store round trip per dword
-            stage_dma(a.pcm, job.pcm_off, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+            stage_dma(a.pcm, job.pcm_off, stg, cw, cst, wave, NW, l, NC == 2 && B == 2, drh, half);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
@@ -1138,8 +1163,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         STAMP(9);
         __syncthreads();
         STAMP(10);
-        if (dbuf && nxt < a.n_jobs)
-            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l, NC == 2 && B == 2);
+        if (dbuf && nxt < n_items)
+            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l, NC == 2 && B == 2, drh, nxt & ssh);
         // The ticket of the frame after next is taken here, behind this frame's wait for its
         // staged PCM, and its value is first used at the estimate barrier (step 9): taken at the
         // top of the loop, the vmcnt(0) for the DMA also waited for the atomic's round trip.
@@ -1751,7 +1776,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // the job record of the frame after next (DMA'd at the top of the next frame)
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         FrameJob jnn{};
-        if (nn < a.n_jobs) jnn = a.jobs[nn];
+        if (nn < n_items) jnn = a.jobs[nn >> ssh];
         uint32_t channel_code, n_out;
         int my_slot;
         if (stereo) {
@@ -1770,9 +1795,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             my_slot = (cand == c0) ? 0 : ((cand == c1) ? 1 : -1);
             n_out = 2;
         } else {
-            channel_code = C - 1u;
-            n_out = C;
-            my_slot = (int)cand;
+            // channel halves: this workgroup holds channels [half C, half C + C) of 2C
+            channel_code = (C << ssh) - 1u;
+            n_out = C << ssh;
+            my_slot = (int)(cand + half * C);
         }
 
         if (tid == 0) {  // frame header (frame_writer.zig:151-265) while the other waves measure
@@ -1883,7 +1909,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
         const uint8_t *pp = par + cur * 512u + ((1u << R.porder) - 1u);
         if (my_slot >= 0) {
-            SubDesc *sd = (SubDesc *)(fd + sizeof(FrameDesc)) + my_slot;
+            SubDesc *sd = (SubDesc *)(fd + sizeof(FrameDesc)) + my_slot;  // (split: the global channel)
             if (l == 0) {
                 sd->type = (uint8_t)R.type;
                 sd->waste = (uint8_t)R.waste;
@@ -1891,7 +1917,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 sd->order = (uint8_t)R.order;
                 sd->porder = (uint8_t)R.porder;
                 sd->method = (uint8_t)R.method;
-                sd->cand = (uint8_t)cand;
+                sd->cand = (uint8_t)(cand + half * C);  // the channel (split: of the whole frame)
                 sd->bits = sub_bits;
                 sd->cval = R.cval;
                 sd->lpc_shift = (int8_t)R.lsh;
@@ -1907,27 +1933,29 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             }
         }
         __syncthreads();  // every written wave's sub_bits
-        if (tid == 0) {
+        if (tid == 0 && half == 0) {
             const uint32_t *hw = misc + 32;
             const uint32_t hb = misc[18];
-            uint32_t total = 8u * hb;
-            for (uint32_t c = 0; c < n_out; c++) total += misc[40 + c];
             FrameDesc *f = (FrameDesc *)fd;
             f->hdr_bytes = hb;
-            f->total_bits = total;
             f->channel_code = channel_code;
             f->n_out = n_out;
             f->hdr[0] = hw[0]; f->hdr[1] = hw[1]; f->hdr[2] = hw[2]; f->hdr[3] = hw[3];
-            const uint32_t fbytes = ((total + 7u) >> 3) + 2u;
-            if (fbytes + 16u > a.image_bytes) atomicOr(a.err, 1u);  // the pack kernel's image bound
-            a.frame_bytes[job.slot] = fbytes;
-            misc[17] = fbytes;
+            if (!ssh) {  // (split: k_frame_totals sums both halves' subframes)
+                uint32_t total = 8u * hb;
+                for (uint32_t c = 0; c < n_out; c++) total += misc[40 + c];
+                f->total_bits = total;
+                const uint32_t fbytes = ((total + 7u) >> 3) + 2u;
+                if (fbytes + 16u > a.image_bytes) atomicOr(a.err, 1u);  // the pack kernel's image bound
+                a.frame_bytes[job.slot] = fbytes;
+                misc[17] = fbytes;
+            }
         }
 
         // ---- 12. optional decision records (parity tests)
         if (a.records) {
             FrameRec *fr = a.records + job.slot;
-            SubRec *sr = &fr->cand[cand];
+            SubRec *sr = &fr->cand[cand + half * C];
             if (l == 0) {
                 sr->type = (uint8_t)R.type;
                 sr->waste = (uint8_t)R.waste;
@@ -1952,10 +1980,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             }
             const uint32_t np = 1u << R.porder;
             for (uint32_t j = l; j < 256u; j += 64) sr->params[j] = (R.type >= 2 && j < np) ? pp[j] : 0;
-            if (tid == 0) {
+            if (tid == 0 && half == 0) {
                 fr->channel_code = channel_code;
-                fr->n_cand = NW;
-                fr->frame_bytes = misc[17];
+                fr->n_cand = NW << ssh;
+                if (!ssh) fr->frame_bytes = misc[17];  // (split: k_frame_totals)
                 fr->pad = 0;
             }
         }

@@ -208,6 +208,26 @@ __global__ void __launch_bounds__(1024) k_scan_blocks(const uint32_t *sizes, uin
 }
 
 // ------------------------------------------------------------------------
+// Frame totals after a channel-split analysis (k_analyze, a.ch_split): the two halves wrote
+// their subframes' descriptors and half 0 the frame header; total bits = header + every
+// subframe, exact frame bytes, the pack kernel's image bound and the records' frame size.
+// ------------------------------------------------------------------------
+__global__ void k_frame_totals(EncodeArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_jobs) return;
+    const uint32_t slot = a.jobs[i].slot;
+    FrameDesc *f = (FrameDesc *)(a.desc + (uint64_t)slot * a.desc_stride);
+    const SubDesc *sd = (const SubDesc *)((const uint8_t *)f + sizeof(FrameDesc));
+    uint32_t total = 8u * f->hdr_bytes;
+    for (uint32_t c = 0; c < f->n_out; c++) total += sd[c].bits;
+    f->total_bits = total;
+    const uint32_t fbytes = ((total + 7u) >> 3) + 2u;
+    if (fbytes + 16u > a.image_bytes) atomicOr(a.err, 1u);
+    a.frame_bytes[slot] = fbytes;
+    if (a.records) a.records[slot].frame_bytes = fbytes;
+}
+
+// ------------------------------------------------------------------------
 // MD5 (md5.zig / RFC 1321): one lane per independent stream
 // ------------------------------------------------------------------------
 constexpr uint32_t kMd5K[64] = {
@@ -433,6 +453,12 @@ hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, 
 hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_advance_jobs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, jobs, n, delta);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_totals(const EncodeArgs &a, hipStream_t st) {
+    if (a.n_jobs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_frame_totals, dim3((a.n_jobs + 255u) / 256u), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
