@@ -2052,6 +2052,11 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
         uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
         const uint32_t n = FULL ? (uint32_t)kBlock : job.n;
+        // single-buffered full frames: the frame's DMA first, so the descriptor's dependent loads
+        // below run under it (the previous frame's last barrier freed the buffer)
+        if constexpr (FULL) {
+            if (!dbuf) stage_dma(a.pcm, job.pcm_off, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+        }
         const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
         const FrameDesc *F = (const FrameDesc *)fd;
         const SubDesc *sd = (const SubDesc *)(fd + sizeof(FrameDesc)) + wave;
@@ -2077,12 +2082,8 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
 
         // ---- 1. PCM -> LDS (already in flight with double buffering), candidate samples -> VGPRs
         STAMP(7);
-        if (dbuf) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if constexpr (FULL) {
-            // one buffer (the frame is too large for two): every wave issues all its LDS-DMA
-            // loads at once and waits once -- not one load-store round trip per dword
-            stage_dma(a.pcm, job.pcm_off, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);
+        if (dbuf || FULL) {
+            // (one buffer: every wave issued all its LDS-DMA loads at the top and waits once)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             stage_sync<FULL>(a.pcm, job.pcm_off, n, C * B, stg, cw, cst, wave, NW, l, NC == 2 && B == 2);

@@ -107,6 +107,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
         uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
+        // single buffer: the frame's DMA first, so the descriptor's dependent loads below run
+        // under it instead of ahead of it (the previous frame's last barrier freed the buffer)
+        if (!dbuf) stage_dma_w(a.pcm, job.pcm_off, stg, cw, cst, dcode, wave, NW, l);
         const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
         const FrameDesc *F = (const FrameDesc *)fd;
         const SubDesc *sd0 = (const SubDesc *)(fd + sizeof(FrameDesc));
@@ -132,12 +135,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
 
         // ---- 1. PCM (double-buffered: DMA'd during the previous frame) -> samples
         STAMP(7);
-        if (dbuf) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            stage_dma_w(a.pcm, job.pcm_off, stg, cw, cst, dcode, wave, NW, l);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP(8);
         __syncthreads();
         STAMP(0);
