@@ -38,7 +38,8 @@ def test_lpc_tails(tail, q):
     check_stream(2, 24, 96000, 4096 + tail, stream=tail, lpc_order=q)
 
 
-@pytest.mark.parametrize("ch,bits,rate,q", [(2, 24, 96000, 8), (2, 32, 192000, 12), (2, 16, 44100, 12)])
+@pytest.mark.parametrize("ch,bits,rate,q", [(2, 24, 96000, 8), (2, 32, 192000, 12), (2, 16, 44100, 12),
+                                            (8, 24, 96000, 8)])  # channel-split analysis
 def test_lpc_decision_records(ch, bits, rate, q):
     _records_match(ch, bits, rate, 4096 * 66 + 333, lpc=q)
 

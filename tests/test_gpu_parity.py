@@ -153,7 +153,9 @@ def _records_match(ch, bits, rate, n, stream=0, lpc=0):
     return got
 
 
-@pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (2, 24, 96000), (2, 32, 192000), (3, 16, 48000)])
+# (8, 24) and (8, 32): full frames analysed in channel halves (two workgroups per frame)
+@pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (2, 24, 96000), (2, 32, 192000), (3, 16, 48000),
+                                         (8, 24, 96000), (8, 32, 192000)])
 def test_decision_records(ch, bits, rate):
     _records_match(ch, bits, rate, 4096 * 66 + 513)
 
