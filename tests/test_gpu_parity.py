@@ -27,6 +27,8 @@ CONFIGS = [
     (1, 32, 48000),
     (8, 32, 192000),  # the largest frame the reference accepts: 8 x 4096 x 4 B
     (7, 16, 44100),
+    (6, 32, 96000),   # channel-split analysis (halves of three 32-bit channels)
+    (4, 24, 48000),   # a 6-byte half row: no split
 ]
 
 _encoders = {}
