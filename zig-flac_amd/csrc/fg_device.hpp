@@ -1843,8 +1843,21 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
 #pragma unroll
                             for (int q = 0; q < LPW; q++)
                                 c[q] = __builtin_amdgcn_readfirstlane(ltab[(k - 1u) * 13u + q]);
-                            residuals_lpc<LPW, int32_t>(x, hs, c, (uint32_t)R.lsh, k, l,
-                                                        [&](int j, bool warm, int64_t e) { f(j, warm, (ST)(int32_t)e); });
+                            // taps bucketed by order (c[t] = 0 past it), as in the order search
+                            auto lpc = [&](auto WT) {
+                                constexpr int W = decltype(WT)::value;
+                                int32_t hsw[W], cw[W];
+#pragma unroll
+                                for (int q = 0; q < W; q++) {
+                                    hsw[q] = hs[q];
+                                    cw[q] = c[q];
+                                }
+                                residuals_lpc<W, int32_t>(x, hsw, cw, (uint32_t)R.lsh, k, l,
+                                                          [&](int j, bool warm, int64_t e) { f(j, warm, (ST)(int32_t)e); });
+                            };
+                            if (k <= 4u) lpc(ic<4>{});
+                            else if (LPW <= 8 || k <= 8u) lpc(ic<(LPW < 8 ? LPW : 8)>{});
+                            else lpc(ic<LPW>{});
                         }
                     } else {
                         SS t[64];
