@@ -14,6 +14,7 @@
 // fg_enc_b{1,2,3,4}.hip.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <type_traits>
 
 #include "fg_common.hpp"
@@ -2371,6 +2372,8 @@ static hipError_t launch_persistent(KernelT k, const EncodeArgs &a, uint32_t thr
     };
     static Occ cache[16];
     static int n_cache = 0, cus = 0;
+    static std::mutex mu;  // contexts on several host threads (fg_multi.cpp) launch concurrently
+    std::lock_guard<std::mutex> lock(mu);
     int resident = 0;
     for (int i = 0; i < n_cache; i++)
         if (cache[i].fn == (const void *)k && cache[i].threads == threads && cache[i].lds == lds)
@@ -2386,7 +2389,7 @@ static hipError_t launch_persistent(KernelT k, const EncodeArgs &a, uint32_t thr
         resident = nb > 0 ? nb : 1;
         if (n_cache < 16) cache[n_cache++] = {(const void *)k, threads, lds, resident};
     }
-    uint64_t grid = a.n_jobs;
+    uint64_t grid = (uint64_t)a.n_jobs << (a.ch_split ? 1 : 0);  // work items (channel halves: two per frame)
     const uint64_t cap = (uint64_t)resident * (uint64_t)(cus > 0 ? cus : 256);
     if (grid > cap) grid = cap;
     if (grid == 0) return hipSuccess;
