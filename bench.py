@@ -88,6 +88,10 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-files", type=int, default=8)
     p.add_argument("--e2e-minutes", type=float, default=10.0)
+    p.add_argument("--no-sharded", action="store_true", help="skip the sharded single-stream line")
+    p.add_argument("--sharded-config", choices=sorted(PRESETS), default="c4")
+    p.add_argument("--sharded-frames", type=int, default=8192, help="frames per rank per window (sharded mode)")
+    p.add_argument("--sharded-steps", type=int, default=10)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-frames", type=int, default=98304, help="blocks in the CPU-baseline sample")
     p.add_argument("--cpu-threads", type=int, default=0, help="0: the CPU share (OMP_NUM_THREADS), capped at a socket")
@@ -148,9 +152,10 @@ class Workload:
         self.d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
         self.d_state = torch.from_numpy(np.frombuffer(flacgpu.md5_states(S), dtype=np.uint8).copy()).to(dev)
         self.md5 = md5
-        self.stream = torch.cuda.current_stream(dev)
+        self.stream = torch.cuda.Stream(dev)  # the encode's own stream (not the legacy null stream)
         self.md5_stream = torch.cuda.Stream(dev)  # in order: each stream's MD5 chain follows the last step's
         self.steps_done = 0
+        torch.cuda.synchronize()  # the buffers above were filled on the default stream
 
     def step(self):
         if self.steps_done:
@@ -163,6 +168,7 @@ class Workload:
 
     def close(self):
         self.plan.close()
+        self.d_pcm = self.d_out = self.d_fb = self.d_off = self.d_tot = self.d_state = None
 
 
 def run_timed(w, steps, warmup, dist=None):
@@ -261,6 +267,116 @@ def read_pmc(key, kernel):
 
 
 # ---------------------------------------------------------------------------------------------
+def sharded_stream(args, rank, world, dist_mod, dev):
+    """BASELINE config 4's data path: ONE long stream, each window's frames sharded over the ranks
+    (rank r: frames [w0 + r F, w0 + (r + 1) F)), every rank's bitstream + sizes gathered by RCCL
+    into one receive buffer on rank 0, STREAMINFO frame-size replay on rank 0's device, all inside
+    the timed region (parallel.ShardedStream).  N = 1 runs the same code as a one-rank RCCL
+    communicator.  The stream's MD5 is one sequential chain and does not shard: it is timed
+    separately on a host core and reported as the Amdahl term, not inside `value`."""
+    import numpy as np
+    import torch
+
+    import flacgpu
+    import parallel
+
+    ch, bits, rate, lpc = PRESETS[args.sharded_config]
+    F = args.sharded_frames
+    fb = ch * (bits // 8)
+    own_group = False
+    if dist_mod is None:
+        import socket
+
+        import torch.distributed as dist_mod
+
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        dist_mod.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                    device_id=dev)
+        own_group = True
+    sub = argparse.Namespace(streams=1, frames=F, channels=ch, bits=bits, rate=rate)
+    shard = build_input(sub, rank)  # this rank's shard of every window (frame numbers move on)
+    enc = flacgpu.Encoder(ch, bits, rate, device=torch.cuda.current_device(), max_frames=F, lpc_order=lpc)
+    d_pcm = torch.from_numpy(shard).to(dev)
+    cstream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(cstream):
+        ss = parallel.ShardedStream(enc, F, dist=dist_mod, device=dev)
+        for _ in range(2):
+            ss.step(d_pcm.data_ptr())
+        torch.cuda.synchronize()
+        enc.reset_timing()
+        enc.set_timing(True)
+        dist_mod.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.sharded_steps):
+            got = ss.step(d_pcm.data_ptr())
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        dist_mod.barrier()
+        enc.set_timing(False)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist_mod.all_reduce(t, op=dist_mod.ReduceOp.MAX)
+    dt = float(t.item())
+    kt = kernel_times(enc)
+    res = None
+    if rank == 0:
+        # proof: rank 0's frames of the last window == the restatement's at the same frame numbers;
+        # the window's device replay == the host replay of its sizes (metadata.zig:35-40)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ref
+
+        body, fsz = got
+        sizes = fsz.cpu().numpy().astype(np.int64)
+        nb0 = int(sizes[:F].sum())
+        last_first = (ss.window - 1) * world * F
+        k = min(F, 64)
+        ref, ref_sizes, _ = oracle_ref.encode_stream(bytes(shard[: k * 4096 * fb]), ch, bits, rate, lpc=lpc,
+                                                     first_frame=last_first)
+        ok = body[: len(ref)].cpu().numpy().tobytes() == ref and [int(x) for x in sizes[:k]] == ref_sizes
+        ok &= int(body.numel()) == int(sizes.sum()) and nb0 > 0
+        mm = torch.tensor([0xFFFFFF, 0], dtype=torch.int32, device=dev)
+        enc.streaminfo_replay_device(fsz.data_ptr(), fsz.numel(), mm.data_ptr())
+        lo, hi = 0xFFFFFF, 0
+        for v in sizes.tolist():
+            if v > hi:
+                hi = v
+            elif v < lo:
+                lo = v
+        ok &= mm.cpu().tolist() == [lo, hi]
+        # the Amdahl term: one stream's MD5 over a window's bytes on one host core
+        sample = shard[: min(len(shard), 64 << 20)].tobytes()
+        t1 = time.perf_counter()
+        hashlib.md5(sample).digest()
+        md5_s = (time.perf_counter() - t1) * (world * len(shard) / len(sample))
+        samples = world * F * 4096 * args.sharded_steps
+        per = {n: round(v[1] / max(v[0], 1), 4) for n, v in kt.items() if v[0]}
+        res = {"workload": f"{args.sharded_config.upper()}: {rate/1000:g}kHz {bits}-bit {ch}ch, ONE stream, "
+                           f"windows of {world} x {F} frames (rank r encodes the r-th {F}), RCCL gather of "
+                           "bitstream + sizes into one rank-0 buffer, STREAMINFO replay on rank 0's device",
+               "ranks": world, "frames_per_rank": F, "windows": args.sharded_steps,
+               "value": round(samples / dt / 1e6, 2), "unit": "MSamples/s",
+               "ms_per_window": round(dt / args.sharded_steps * 1e3, 4),
+               "kernel_ms_per_window": per,
+               "gather": "all_gather of (frames, bytes) counts, then batched point-to-point RCCL transfers into "
+                         "slices of one receive buffer (rank 0 encodes into its head in place)",
+               "md5_amdahl": {"ms_per_window_one_host_core": round(md5_s * 1e3, 2),
+                              "stream_cap_msamples_per_s": round(world * F * 4096 / md5_s / 1e6, 1),
+                              "note": "one stream's MD5 is a serial chain over every window (wav_reader.zig:66): "
+                                      "it does not shard and is not in `value`"},
+               "output_ok": bool(ok),
+               "verified": f"rank 0's first {k} frames of the last window (frame numbers from {last_first}) vs "
+                           "the restatement; device STREAMINFO replay of the window vs the host replay"}
+    ss.close()
+    enc.close()
+    del d_pcm
+    if own_group:
+        dist_mod.destroy_process_group()
+    return res
+
+
 def stream_curve(args, enc, d_pcm, fb, dev):
     """Same blocks per step at S concurrent streams: encode vs the per-stream MD5 chain."""
     out = []
@@ -393,23 +509,14 @@ def socket0_cpus():
         return sorted(os.sched_getaffinity(0))
 
 
-def cpu_baseline(buf, args):
-    """The CPU restatement (oracle/, built -O3 -march=x86-64-v4 as liboracle_fast.so) on P
-    threads pinned to distinct cores of socket 0, each encoding whole streams (incl. MD5)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ref
-
-    L = oracle_ref.lib(fast=True)
-    facts = cpu_facts()
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    P = args.cpu_threads or min(share, facts["cores_per_socket"] or share)
-    cpus = socket0_cpus()
+def _cpu_run(L, oracle_ref, buf, args, P, frames, cpus, lpc):
+    """P pinned threads, each encoding whole 8-block streams (incl. MD5) of `buf`; -> (samples, s)."""
     ch, bits = args.channels, args.bits
     fb = ch * (bits // 8)
     per_stream = 8 * 4096  # 8-block streams, the headline's shape
     n_streams_buf = len(buf) // (per_stream * fb)
-    per_thread = max(1, args.cpu_frames // P // 8)
-    cfg = oracle_ref.config(ch, bits, args.rate, lpc=args.lpc)
+    per_thread = max(1, frames // P // 8)
+    cfg = oracle_ref.config(ch, bits, args.rate, lpc=lpc)
     res = [0] * P
     cap = 8 * L.oracle_max_frame_bytes(4096, bits, ch) + 64
 
@@ -436,8 +543,38 @@ def cpu_baseline(buf, args):
         t.start()
     for t in th:
         t.join()
-    dt = time.perf_counter() - t0
-    tot = sum(res)
+    return sum(res), time.perf_counter() - t0
+
+
+def cpu_baseline(buf, args):
+    """The CPU restatement (oracle/, built -O3 -march=x86-64-v4 as liboracle_fast.so): one thread
+    (one core, the reference's own shape: wav2flac is single-threaded) and P threads pinned to
+    distinct socket-0 cores, each encoding whole streams (incl. MD5).  LPC configs are also run
+    fixed-only, which is what the reference (no LPC, readme.md:27) does on the same input."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref
+
+    L = oracle_ref.lib(fast=True)
+    facts = cpu_facts()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    P = args.cpu_threads or min(share, facts["cores_per_socket"] or share)
+    cpus = socket0_cpus()
+    try:
+        main_aff = os.sched_getaffinity(0)
+    except Exception:
+        main_aff = None
+    tot1, dt1 = _cpu_run(L, oracle_ref, buf, args, 1, max(8, args.cpu_frames // 8), cpus, args.lpc)
+    tot, dt = _cpu_run(L, oracle_ref, buf, args, P, args.cpu_frames, cpus, args.lpc)
+    fixed_only = None
+    if args.lpc:
+        totf, dtf = _cpu_run(L, oracle_ref, buf, args, P, args.cpu_frames, cpus, 0)
+        fixed_only = {"value": round(totf / dtf / 1e6, 3), "cores": P,
+                      "note": "LPC off: the reference's own encoding of this input (it has no LPC)"}
+    if main_aff:
+        try:
+            os.sched_setaffinity(0, main_aff)
+        except Exception:
+            pass
     value = tot / dt / 1e6
     cps = facts["cores_per_socket"]
     return {
@@ -445,8 +582,12 @@ def cpu_baseline(buf, args):
         "unit": "MSamples/s",
         "cores": P,
         "kind": "port",
-        "sample": f"{tot} samples ({tot // 4096} blocks as {P * per_thread} 8-block streams, incl. MD5), "
+        "sample": f"{tot} samples ({tot // 4096} blocks as 8-block streams, incl. MD5), "
                   f"{P} threads pinned to socket-0 cores, {dt:.2f}s wall ({dt * P:.1f} CPU-s)",
+        "single_core": {"value": round(tot1 / dt1 / 1e6, 3), "cores": 1,
+                        "sample": f"{tot1} samples ({tot1 // 4096} blocks), one thread on one core, {dt1:.2f}s"},
+        "fixed_only": fixed_only,
+        "lpc": args.lpc,
         "cpu_model": facts["model"],
         "cores_per_socket": cps,
         "sockets": facts["sockets"],
@@ -454,8 +595,9 @@ def cpu_baseline(buf, args):
                  "unbuildable here: no Zig 0.16 on the box)",
         "per_core": round(value / P, 3),
         "single_socket_estimate": round(value / P * cps, 1) if cps else None,
-        "single_socket_note": f"P = {P} (the box's CPU share for one GPU) of {cps} cores per socket were run; "
-                              "the socket figure scales the measured per-core rate linearly (an upper bound)",
+        "single_socket_note": f"measured at P = {P} threads (the box's CPU share for one GPU) of {cps} cores per "
+                              "socket; the socket figure scales the measured per-core rate linearly (an ESTIMATE, "
+                              "an upper bound: memory bandwidth and clocks are shared)",
     }
 
 
@@ -522,6 +664,14 @@ def main():
     ok, vinfo = verify(args, w, buf, fb, args.verify_streams, dev) if rank == 0 else (True, {})
     w.close()
 
+    sharded = None
+    if not args.no_sharded:
+        del d_pcm
+        torch.cuda.empty_cache()
+        sharded = sharded_stream(args, rank, world, dist, dev)
+        d_pcm = torch.from_numpy(buf).to(dev) if (rank == 0 and world == 1 and not args.no_curve
+                                                  and not args.no_md5) else None
+
     curve = e2e = cpu = None
     if rank == 0 and world == 1:
         if not args.no_curve and not args.no_md5:
@@ -584,6 +734,7 @@ def main():
             "output_ok": ok,
             "verified": vinfo,
             "stream_curve": curve,
+            "sharded_stream": sharded,
             "end_to_end": e2e,
             "cpu_baseline": cpu,
         }

@@ -15,6 +15,12 @@
  *
  * Threading: one context per GPU per host thread; a context is not
  * thread-safe.  All functions return FLACGPU_OK (0) or a negative error code.
+ *
+ * Streams: `void *hip_stream` is a hipStream_t passed through to HIP unchanged,
+ * except NULL, which selects the context's own (non-blocking) stream.  The HIP
+ * null stream is NOT NULL here: pass FLACGPU_STREAM_LEGACY (== hipStreamLegacy)
+ * to order the work against legacy-default-stream work (e.g. a framework whose
+ * current stream handle is 0).
  */
 #ifndef FLACGPU_H
 #define FLACGPU_H
@@ -27,6 +33,9 @@ extern "C" {
 #endif
 
 #define FLACGPU_ABI_VERSION 3
+
+/* the legacy null stream as a hip_stream argument (== hipStreamLegacy) */
+#define FLACGPU_STREAM_LEGACY ((void *)1)
 
 /* Error codes (map to the Zig error set
  * {OutOfMemory, WriteFailed, DeviceError, InvalidConfig, InvalidInput}). */
@@ -167,7 +176,9 @@ int flacgpu_plan_advance(flacgpu_plan *plan, uint64_t frames, void *hip_stream);
 typedef struct {
     uint32_t h[4];      /* MD5 chaining value */
     uint64_t bytes;     /* message bytes absorbed */
-    uint32_t finished;  /* 1 once the final segment has been padded */
+    uint32_t finished;  /* 1 once the final segment has been padded: h is then the digest, and
+                           later calls leave the state unchanged (a final segment passed again
+                           reports the same digest); re-initialise it to start a new stream */
     uint32_t reserved;
 } flacgpu_md5_state;
 void flacgpu_md5_state_init(flacgpu_md5_state *states, size_t n);
@@ -251,6 +262,14 @@ void flacgpu_streaminfo_init(flacgpu_streaminfo *si, uint32_t sample_rate, uint3
                              uint64_t interchannel_samples, uint32_t block_size);
 /* StreamInfo.updateFrameSize (metadata.zig:35-40), with its else-if. */
 void flacgpu_streaminfo_update_frame_size(flacgpu_streaminfo *si, uint32_t frame_size);
+/* StreamInfo.updateFrameSize replayed over n_frames device-resident frame sizes in frame
+ * order (metadata.zig:35-40, the caller's loop at wav2flac.zig:94): d_minmax (device, u32[2])
+ * holds {min_frame_size, max_frame_size} on entry (0xFFFFFF, 0 for a new stream, or the
+ * state after earlier windows) and on exit, with the reference's else-if quirk: a frame that
+ * raises the running max never lowers the min.  One workgroup, queued on hip_stream; the
+ * bitstream of a sharded encode never leaves HBM for its STREAMINFO. */
+int flacgpu_streaminfo_replay_device(flacgpu_ctx *ctx, const uint32_t *d_frame_bytes, uint64_t n_frames,
+                                     uint32_t *d_minmax, void *hip_stream);
 /* StreamInfo.bytes (metadata.zig:42-68). */
 void flacgpu_streaminfo_bytes(const flacgpu_streaminfo *si, uint8_t out[34]);
 /* Encoder.writeHeader (encoder.zig:192-206): "fLaC" + STREAMINFO block; returns 42. */

@@ -27,6 +27,46 @@ class OracleFrames:
         return out, sizes
 
 
+def run_windows(a, enc, dist, device):
+    """parallel.ShardedStream over a stream of windows x world x F whole frames: each rank holds
+    only its shard of each window; rank 0 assembles the file (the bench's C4 sharded mode)."""
+    import ctypes
+    import hashlib
+
+    import numpy as np
+    import torch
+
+    import flacgpu
+    import parallel
+    import synth
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    F, B = a.frames_per_rank, 4096
+    per = a.channels * (a.bits // 8)
+    n = a.windows * world * F * B
+    pcm = synth.synth_pcm(n, a.channels, a.bits, a.rate)
+    ss = parallel.ShardedStream(enc, F, dist=dist, device=device)
+    body = []
+    for w in range(a.windows):
+        s0 = (w * world + rank) * F * B
+        shard = pcm[s0 * per:(s0 + F * B) * per]
+        if ss.gpu:
+            d = torch.from_numpy(np.frombuffer(shard, dtype=np.uint8).copy()).to(device)
+            got = ss.step(d.data_ptr())
+        else:
+            got = ss.step(shard)
+        if rank == 0:
+            body.append(got[0].cpu().numpy().tobytes())
+    ss.close()
+    if rank != 0:
+        return None
+    lo, hi = ss.frame_size_minmax()
+    si = flacgpu.StreamInfo.new(a.rate, a.channels, a.bits, n, B)
+    si.min_frame_size, si.max_frame_size = lo, hi
+    ctypes.memmove(si.md5, hashlib.md5(pcm).digest(), 16)
+    return flacgpu.header_bytes(si, False) + flacgpu.vorbis_comment_bytes(True) + b"".join(body)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--encoder", choices=["oracle", "gpu"], default="oracle")
@@ -37,6 +77,10 @@ def main():
     p.add_argument("--md5", default="host")
     p.add_argument("--backend", choices=["gloo", "nccl"], default="gloo")
     p.add_argument("--out", required=True)
+    p.add_argument("--mode", choices=["file", "windows"], default="file",
+                   help="file: parallel.encode_sharded; windows: parallel.ShardedStream over --windows windows")
+    p.add_argument("--windows", type=int, default=3)
+    p.add_argument("--frames-per-rank", type=int, default=2)
     a = p.parse_args()
     import torch.distributed as dist
 
@@ -58,10 +102,13 @@ def main():
         import flacgpu
 
         enc = flacgpu.Encoder(a.channels, a.bits, a.rate, device=torch.cuda.current_device() if a.backend == "nccl"
-                              else 0, max_frames=256)
+                              else 0, max_frames=max(256, a.frames_per_rank))
     else:
         enc = OracleFrames(a.channels, a.bits, a.rate)
-    out = parallel.encode_sharded(enc, pcm, dist=dist, device=device, md5=a.md5)
+    if a.mode == "windows":
+        out = run_windows(a, enc, dist, device)
+    else:
+        out = parallel.encode_sharded(enc, pcm, dist=dist, device=device, md5=a.md5)
     if dist.get_rank() == 0:
         open(a.out, "wb").write(out)
     dist.barrier()

@@ -179,6 +179,8 @@ def test_streams_spanning_calls_carry_md5_state(ch, bits, rate):
                                    states=state)
             for s, (got, sz, dig) in enumerate(res):
                 if digest[s] is not None:
+                    # a finished state passed again is left as it is: the same digest, no re-padding
+                    assert dig == digest[s], f"stream {s}: finished MD5 state changed"
                     continue
                 outs[s] += got
                 sizes[s] += sz
@@ -269,3 +271,29 @@ def test_plan_scan_spans_blocks(misalign):
     ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, ch, bits, rate, block=bs)
     assert [int(x) for x in sizes] == ref_sizes
     assert d_out[:total].cpu().numpy().tobytes() == ref
+
+
+def test_default_stream_producer_is_ordered():
+    """d_pcm written by a GPU kernel on torch's default (legacy null) stream and encoded at once
+    through stream handle 0: the wrapper passes FLACGPU_STREAM_LEGACY, so the encode is queued
+    behind the producer (and behind the default-stream zero-fill of the result buffers) instead of
+    running unordered on the context's non-blocking stream."""
+    torch, dev = _torch()
+    import flacgpu
+
+    n = 48 * 4096 + 333
+    pcm = synth.synth_pcm(n, 2, 16, 44100, stream=77)
+    key = 0x5A
+    src = torch.from_numpy(np.frombuffer(pcm, dtype=np.uint8) ^ np.uint8(key)).to(dev)
+    torch.cuda.synchronize()
+    assert torch.cuda.current_stream(dev).cuda_stream == 0
+    a = torch.randn(4096, 4096, device=dev)
+    for _ in range(6):  # keep the default stream busy for a while before the producer runs
+        a = (a @ a) * 1e-3
+    d_pcm = torch.bitwise_xor(src, key)  # the producer kernel, queued behind the matmuls
+    with flacgpu.Encoder(2, 16, 44100, max_frames=64) as enc:
+        frames, sizes = enc.encode_frames_device(d_pcm.data_ptr(), n)  # current stream: handle 0
+        got, got_sizes = frames.cpu().numpy().tobytes(), [int(x) for x in sizes.cpu()]
+    ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, 2, 16, 44100)
+    assert got_sizes == ref_sizes and got == ref
+    assert flacgpu._stream(0) == flacgpu.STREAM_LEGACY and flacgpu._stream(None) is None

@@ -85,3 +85,27 @@ def test_sharded_gpu_rccl_device_gather(tmp_path, nproc, n):
     out = run_workers(tmp_path, nproc, "--encoder", "gpu", "--backend", "nccl", "--samples", str(n))
     pcm = synth.synth_pcm(n, 2, 16, 44100)
     assert out == oracle_ref.encode_file(pcm, 2, 16, 44100)
+
+
+@pytest.mark.parametrize("nproc,ch,bits,windows,f", [(2, 2, 16, 3, 2), (2, 8, 24, 2, 1), (3, 1, 16, 2, 3)])
+def test_sharded_stream_windows_gloo(tmp_path, nproc, ch, bits, windows, f):
+    """parallel.ShardedStream (the bench's sharded-stream mode) on world_size > 1 with gloo:
+    each rank encodes only its shard of each window, rank 0 gathers in frame order and carries
+    the STREAMINFO frame-size replay across windows; the file equals the whole-file encode."""
+    out = run_workers(tmp_path, nproc, "--encoder", "oracle", "--mode", "windows", "--channels", str(ch),
+                      "--bits", str(bits), "--windows", str(windows), "--frames-per-rank", str(f))
+    n = windows * nproc * f * 4096
+    pcm = synth.synth_pcm(n, ch, bits, 44100)
+    assert out == oracle_ref.encode_file(pcm, ch, bits, 44100)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ch,bits", [(2, 16), (8, 24)])
+def test_sharded_stream_windows_rccl_one_rank(tmp_path, ch, bits):
+    """The same ShardedStream on the GPU: device plan advanced window to window, rank 0 encodes
+    into its receive buffer, one-rank RCCL communicator, STREAMINFO replayed on the device."""
+    out = run_workers(tmp_path, 1, "--encoder", "gpu", "--backend", "nccl", "--mode", "windows", "--channels",
+                      str(ch), "--bits", str(bits), "--windows", "3", "--frames-per-rank", "5")
+    n = 3 * 5 * 4096
+    pcm = synth.synth_pcm(n, ch, bits, 44100)
+    assert out == oracle_ref.encode_file(pcm, ch, bits, 44100)

@@ -30,6 +30,7 @@ hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const u
                               uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st);
 hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipStream_t st);
 hipError_t launch_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks, hipStream_t st);
+hipError_t launch_streaminfo_replay(const uint32_t *sizes, uint64_t n, uint32_t *minmax, hipStream_t st);
 }  // namespace fg
 
 using namespace fg;
@@ -999,6 +1000,15 @@ int flacgpu_encode_plan_device(flacgpu_ctx *c, const flacgpu_plan *p, const void
                                uint8_t *d_md5, void *hip_stream) {
     return flacgpu_encode_plan_device_ex(c, p, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total, nullptr,
                                          d_md5, hip_stream, nullptr);
+}
+
+int flacgpu_streaminfo_replay_device(flacgpu_ctx *c, const uint32_t *d_frame_bytes, uint64_t n_frames,
+                                     uint32_t *d_minmax, void *hip_stream) {
+    if (!c || !d_minmax || (n_frames && !d_frame_bytes)) return FLACGPU_ERR_INVALID_INPUT;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    HIPCHK(launch_streaminfo_replay(d_frame_bytes, n_frames, d_minmax, st));
+    return FLACGPU_OK;
 }
 
 int flacgpu_sync_check(flacgpu_ctx *c, void *hip_stream) {

@@ -2362,32 +2362,45 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
 #include "fg_pack4.hpp"
 #include "fg_packw.hpp"
 
-// persistent launch: grid = min(frames, resident workgroups)
+// persistent launch: grid = min(work items, resident workgroups on this device).  The occupancy
+// is cached per (kernel, threads, LDS, device); the lock covers only the cache lookup/insert, so
+// contexts driven from several host threads (fg_multi.cpp) launch concurrently.  A miss computes
+// outside the lock (two racing threads compute the same value).
 template <typename KernelT>
 static hipError_t launch_persistent(KernelT k, const EncodeArgs &a, uint32_t threads, uint32_t lds, hipStream_t st) {
     struct Occ {
         const void *fn;
         uint32_t threads, lds;
-        int resident;
+        int device, resident, cus;
     };
-    static Occ cache[16];
-    static int n_cache = 0, cus = 0;
-    static std::mutex mu;  // contexts on several host threads (fg_multi.cpp) launch concurrently
-    std::lock_guard<std::mutex> lock(mu);
-    int resident = 0;
-    for (int i = 0; i < n_cache; i++)
-        if (cache[i].fn == (const void *)k && cache[i].threads == threads && cache[i].lds == lds)
-            resident = cache[i].resident;
+    static Occ cache[64];
+    static int n_cache = 0;
+    static std::mutex mu;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    int resident = 0, cus = 0;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        for (int i = 0; i < n_cache; i++)
+            if (cache[i].fn == (const void *)k && cache[i].threads == threads && cache[i].lds == lds &&
+                cache[i].device == dev) {
+                resident = cache[i].resident;
+                cus = cache[i].cus;
+                break;
+            }
+    }
     if (!resident) {
-        hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
-        int dev = 0, nb = 0;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        int nb = 0;
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k, (int)threads, (size_t)lds);
         if (e != hipSuccess) return e;
         resident = nb > 0 ? nb : 1;
-        if (n_cache < 16) cache[n_cache++] = {(const void *)k, threads, lds, resident};
+        std::lock_guard<std::mutex> lock(mu);
+        if (n_cache < 64) cache[n_cache++] = {(const void *)k, threads, lds, dev, resident, cus};
     }
     uint64_t grid = (uint64_t)a.n_jobs << (a.ch_split ? 1 : 0);  // work items (channel halves: two per frame)
     const uint64_t cap = (uint64_t)resident * (uint64_t)(cus > 0 ? cus : 256);

@@ -228,6 +228,56 @@ __global__ void k_frame_totals(EncodeArgs a) {
 }
 
 // ------------------------------------------------------------------------
+// StreamInfo.updateFrameSize over device-resident sizes (metadata.zig:35-40):
+//   if (sz > max) max = sz; else if (sz < min) min = sz;
+// in frame order.  max ends as the plain maximum; frame f can lower min only when it does
+// not raise the max, i.e. when sz_f <= M_f = max(max_in, sz_0 .. sz_{f-1}).  So
+// min = min(min_in, min{ sz_f : sz_f <= M_f }).  Thread t owns a contiguous run of frames:
+// run maxima -> exclusive max-scan across the workgroup -> each run replayed from its M.
+// ------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_streaminfo_replay(const uint32_t *sizes, uint64_t n, uint32_t *minmax) {
+    __shared__ uint32_t wmax[16], wmin[16];
+    const uint32_t t = threadIdx.x, l = lane_id_m(), w = t >> 6;
+    const uint64_t per = (n + 1023u) / 1024u;
+    const uint64_t b = (uint64_t)t * per, e = b + per < n ? b + per : n;
+    const uint32_t min_in = minmax[0], max_in = minmax[1];
+    uint32_t rmax = 0;
+    for (uint64_t i = b; i < e; i++) rmax = max(rmax, sizes[i]);
+    // inclusive max-scan within the wave, then across waves
+    uint32_t x = rmax;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (l >= (uint32_t)d) x = max(x, y);
+    }
+    if (l == 63) wmax[w] = x;
+    __syncthreads();
+    uint32_t before = max_in, all = max_in;
+    for (uint32_t i = 0; i < 16; i++) {
+        all = max(all, wmax[i]);
+        if (i < w) before = max(before, wmax[i]);
+    }
+    const uint32_t excl = __shfl_up(x, 1);
+    uint32_t M = l ? max(before, excl) : before;  // running max entering this thread's run
+    uint32_t mn = 0xFFFFFFFFu;
+    for (uint64_t i = b; i < e; i++) {
+        const uint32_t sz = sizes[i];
+        if (sz > M) M = sz;
+        else mn = min(mn, sz);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mn = min(mn, __shfl_xor(mn, d));
+    if (l == 0) wmin[w] = mn;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t m = min_in;
+        for (int i = 0; i < 16; i++) m = min(m, wmin[i]);
+        minmax[0] = m;
+        minmax[1] = all;
+    }
+}
+
+// ------------------------------------------------------------------------
 // MD5 (md5.zig / RFC 1321): one lane per independent stream
 // ------------------------------------------------------------------------
 constexpr uint32_t kMd5K[64] = {
@@ -357,6 +407,15 @@ __global__ void __launch_bounds__(kMd5Wg) __attribute__((amdgpu_waves_per_eu(FG_
         st[2] = in.h[2];
         st[3] = in.h[3];
         done = in.bytes;
+        if (in.flags & 1u) {
+            // already finalised (Md5.final ran, encoder.zig:168-170): h IS the digest.  Absorbing
+            // more bytes or padding again would corrupt it, so the state is left as it is and a
+            // requested digest is the finished one (re-initialise a state before reusing it)
+            if (fin && digests)
+                for (int i = 0; i < 4; i++)
+                    for (int j = 0; j < 4; j++) digests[16 * s + 4 * i + j] = (uint8_t)(st[i] >> (8 * j));
+            return;
+        }
     }
     const uint64_t full = len >> 6;
     // ring of kMd5Ahead + 1 message blocks: block b is consumed while b + 1 .. b + kMd5Ahead load
@@ -472,6 +531,12 @@ hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total
     const uint32_t nb = (n + kScanBlock - 1u) / kScanBlock;
     if (nb > 1u) hipLaunchKernelGGL(k_scan_part, dim3(nb), dim3(1024), 0, st, sizes, part, n);
     hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, sizes, offsets, total, part, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_streaminfo_replay(const uint32_t *sizes, uint64_t n, uint32_t *minmax, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_streaminfo_replay, dim3(1), dim3(1024), 0, st, sizes, n, minmax);
     return hipGetLastError();
 }
 

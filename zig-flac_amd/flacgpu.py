@@ -199,6 +199,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_plan_advance": (I32, [P, U64, P]),
         "flacgpu_encode_plan_device_ex": (I32, [P, P, P, P, U64, P, P, P, P, P, P, P]),
         "flacgpu_sync_check": (I32, [P, P]),
+        "flacgpu_streaminfo_replay_device": (I32, [P, P, U64, P, P]),
         "flacgpu_md5_set_engine": (I32, [P, I32]),
         "flacgpu_md5_get_engine": (I32, [P]),
         "flacgpu_md5_state_init": (None, [P, SZ]),
@@ -242,6 +243,7 @@ def exported_symbols() -> list:
         "flacgpu_plan_create", "flacgpu_plan_destroy", "flacgpu_plan_frames", "flacgpu_plan_out_bound",
         "flacgpu_plan_stream_first_frame", "flacgpu_encode_plan_device", "flacgpu_encode_plan_device_md5_async",
         "flacgpu_plan_create_segments", "flacgpu_plan_advance", "flacgpu_encode_plan_device_ex", "flacgpu_sync_check",
+        "flacgpu_streaminfo_replay_device",
         "flacgpu_md5_set_engine", "flacgpu_md5_get_engine", "flacgpu_md5_state_init",
         "flacgpu_set_timing",
         "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_get_records",
@@ -249,6 +251,18 @@ def exported_symbols() -> list:
         "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file",
         "flacgpu_wav_to_flac", "flacgpu_open_multi", "flacgpu_close_multi", "flacgpu_multi_encode_frames",
     ]
+
+
+STREAM_LEGACY = 1  # FLACGPU_STREAM_LEGACY == hipStreamLegacy
+
+
+def _stream(h: Optional[int]) -> Optional[int]:
+    """A torch/HIP stream handle as the C ABI's `void *hip_stream`: None -> NULL (the context's
+    own non-blocking stream); 0 (the legacy null stream, torch's default) -> FLACGPU_STREAM_LEGACY,
+    so the work stays ordered against default-stream producers and consumers."""
+    if h is None:
+        return None
+    return STREAM_LEGACY if h == 0 else h
 
 
 def _check(rc: int, where: str) -> None:
@@ -278,7 +292,7 @@ class Plan:
 
     def advance(self, frames: int, stream: Optional[int] = None) -> None:
         """flacgpu_plan_advance: the next window of the same streams (frame numbers + frames)."""
-        _check(self.enc.lib.flacgpu_plan_advance(self.handle, frames, stream or None), "plan_advance")
+        _check(self.enc.lib.flacgpu_plan_advance(self.handle, frames, _stream(stream)), "plan_advance")
 
     def close(self) -> None:
         if self.handle:
@@ -382,6 +396,12 @@ class Encoder:
     def set_md5_engine(self, engine: int) -> None:
         _check(self.lib.flacgpu_md5_set_engine(self.ctx, engine), "md5_set_engine")
 
+    def md5_engine(self) -> int:
+        e = self.lib.flacgpu_md5_get_engine(self.ctx)
+        if e < 0:
+            raise FlacGpuError(e, "md5_get_engine")
+        return e
+
     def md5(self, data: bytes) -> bytes:
         _check(self.lib.flacgpu_md5_init(self.ctx), "md5_init")
         buf = ctypes.create_string_buffer(bytes(data), len(data))
@@ -411,11 +431,18 @@ class Encoder:
         """flacgpu_encode_plan_device_ex: MD5 state carried in d_md5_state (32 B per stream)."""
         _check(self.lib.flacgpu_encode_plan_device_ex(
             self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total,
-            d_md5_state or None, d_md5 or None, stream or None, md5_stream or None), "encode_plan_device_ex")
+            d_md5_state or None, d_md5 or None, _stream(stream), _stream(md5_stream)), "encode_plan_device_ex")
 
     def sync_check(self, stream: Optional[int] = None) -> None:
         """Synchronise `stream` and raise if a kernel flagged a device-side error."""
-        _check(self.lib.flacgpu_sync_check(self.ctx, stream or None), "sync_check")
+        _check(self.lib.flacgpu_sync_check(self.ctx, _stream(stream)), "sync_check")
+
+    def streaminfo_replay_device(self, d_frame_bytes: int, n_frames: int, d_minmax: int,
+                                 stream: Optional[int] = None) -> None:
+        """StreamInfo.updateFrameSize (metadata.zig:35-40) over device frame sizes; d_minmax = u32
+        {min, max} in/out on the device ({0xFFFFFF, 0} for a new stream)."""
+        _check(self.lib.flacgpu_streaminfo_replay_device(self.ctx, d_frame_bytes, n_frames, d_minmax,
+                                                         _stream(stream)), "streaminfo_replay_device")
 
     def encode_frames_device(self, d_pcm: int, n_samples: int, first_frame: int = 0, stream: Optional[int] = None):
         """Frames of n_samples interleaved samples at device address d_pcm, numbered from first_frame, kept in
@@ -446,10 +473,10 @@ class Encoder:
         if md5_stream:
             _check(self.lib.flacgpu_encode_plan_device_md5_async(
                 self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total,
-                d_md5 or None, stream or None, md5_stream), "encode_plan_device_md5_async")
+                d_md5 or None, _stream(stream), _stream(md5_stream)), "encode_plan_device_md5_async")
             return
         _check(self.lib.flacgpu_encode_plan_device(self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes,
-                                                   d_frame_offsets, d_total, d_md5 or None, stream or None),
+                                                   d_frame_offsets, d_total, d_md5 or None, _stream(stream)),
                "encode_plan_device")
 
     # ---- instrumentation
