@@ -86,7 +86,7 @@ def parse():
     p.add_argument("--no-curve", action="store_true")
     p.add_argument("--curve", default="8,64,1024,8192,16384")
     p.add_argument("--no-e2e", action="store_true")
-    p.add_argument("--e2e-files", type=int, default=8)
+    p.add_argument("--e2e-files", default="8,16,32", help="file counts of the end-to-end curve")
     p.add_argument("--e2e-minutes", type=float, default=10.0)
     p.add_argument("--no-sharded", action="store_true", help="skip the sharded single-stream line")
     p.add_argument("--sharded-config", choices=sorted(PRESETS), default="c4")
@@ -397,20 +397,30 @@ def stream_curve(args, enc, d_pcm, fb, dev):
 
 
 def end_to_end(args):
-    """BASELINE.md end-to-end contract: host PCM buffers -> .flac files in host memory."""
+    """BASELINE.md end-to-end contract: host PCM buffers -> .flac files in host memory, as a curve
+    over the number of files encoded at once (one context + one host thread per file, each file's
+    MD5 on its own host thread beside its GPU encode), from pinned staging buffers."""
     import numpy as np
+    import torch
+
     import flacgpu
     import synth
 
     ch, bits, rate = 2, 16, 44100
     n = int(args.e2e_minutes * 60 * rate)
     fb = ch * 2
+    counts = sorted({int(x) for x in str(args.e2e_files).split(",") if x})
+    nmax = max(counts)
     pool_n = 4096 * 1024
     pool = np.frombuffer(synth.to_pcm_bytes(synth.synth_samples(pool_n, ch, bits, rate, stream=11), bits),
                          dtype=np.uint8)
+
+    def pinned(nbytes):
+        return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
+
     files = []
-    for i in range(args.e2e_files):
-        buf = np.empty(n * fb, dtype=np.uint8)
+    for i in range(nmax):
+        buf = pinned(n * fb)
         pos, k = 0, i
         while pos < n:
             take = min(n - pos, pool_n - 4096 * (k % 64))
@@ -422,16 +432,16 @@ def end_to_end(args):
     L = flacgpu.load_library()
     encs = [flacgpu.Encoder(ch, bits, rate, device=0, max_frames=4096) for _ in files]
     cap = 200 + ((n + 4095) // 4096 + 1) * encs[0].frame_bound()
-    outs = [np.empty(cap, dtype=np.uint8) for _ in files]
+    outs = [pinned(cap) for _ in files]
     lens = [ctypes.c_size_t(0) for _ in files]
-    rcs = [0] * len(files)
+    rcs = [0] * nmax
 
     def one(i):
         rcs[i] = L.flacgpu_encode_file(encs[i].ctx, files[i].ctypes.data_as(ctypes.c_void_p), 2, n,
                                        outs[i].ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(lens[i]))
 
-    def run_all():
-        th = [threading.Thread(target=one, args=(i,)) for i in range(len(files))]
+    def run_all(nf):
+        th = [threading.Thread(target=one, args=(i,)) for i in range(nf)]
         t0 = time.perf_counter()
         for t in th:
             t.start()
@@ -439,27 +449,29 @@ def end_to_end(args):
             t.join()
         return time.perf_counter() - t0
 
-    run_all()
-    best = min(run_all() for _ in range(2))
-    ok = all(r == 0 for r in rcs)
-    # parts, measured alone: one file's MD5 on one host core; all files' encodes without MD5
+    run_all(min(nmax, 8))
+    curve = []
+    for nf in counts:
+        best = min(run_all(nf) for _ in range(2))
+        curve.append({"files": nf, "value": round(nf * n / best / 1e6, 1), "wall_ms": round(best * 1e3, 2),
+                      "ok": all(r == 0 for r in rcs[:nf])})
+    ok = all(c["ok"] for c in curve)
+    # bounds: one file's MD5 on one host core; pinned H2D bandwidth
     t0 = time.perf_counter()
     hashlib.md5(files[0]).digest()
     md5_s = time.perf_counter() - t0
-    frames_caps = [np.empty(cap, dtype=np.uint8) for _ in files]
-
-    def enc_only(i):
-        ol = ctypes.c_size_t(0)
-        L.flacgpu_encode_frames(encs[i].ctx, files[i].ctypes.data_as(ctypes.c_void_p), 2, n, 0,
-                                frames_caps[i].ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(ol), None)
-
-    th = [threading.Thread(target=enc_only, args=(i,)) for i in range(len(files))]
+    d = torch.empty(len(files[0]), dtype=torch.uint8, device="cuda")
+    src = torch.from_numpy(files[0])
+    d.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    enc_s = time.perf_counter() - t0
+    for _ in range(4):
+        d.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d_gbs = 4 * len(files[0]) / (time.perf_counter() - t0) / 1e9
+    del d
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    md5_gbs = len(files[0]) / md5_s / 1e9
     # proof: file 0 is byte-identical to the restatement's whole-file encode (header, MD5, frames)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref
@@ -468,13 +480,17 @@ def end_to_end(args):
     ok &= outs[0][: lens[0].value].tobytes() == ref
     for e in encs:
         e.close()
-    total = n * len(files)
-    return {"files": len(files), "minutes_per_file": args.e2e_minutes, "samples": total,
-            "value": round(total / best / 1e6, 1), "unit": "MSamples/s", "wall_ms": round(best * 1e3, 2),
-            "md5_one_file_host_core_ms": round(md5_s * 1e3, 2), "encode_only_all_files_ms": round(enc_s * 1e3, 2),
-            "path": "pageable host PCM -> flacgpu_encode_file per file (one context + host thread each): "
-                    "H2D, kernels, D2H pipelined in 2048-frame chunks; MD5 on a host thread per file beside "
-                    "the encode; 73-byte header + frames in host memory",
+    top = max(curve, key=lambda c: c["value"])
+    return {"files": top["files"], "minutes_per_file": args.e2e_minutes, "samples": top["files"] * n,
+            "value": top["value"], "unit": "MSamples/s", "wall_ms": top["wall_ms"], "curve": curve,
+            "md5_one_file_host_core_ms": round(md5_s * 1e3, 2),
+            "bounds_msamples_per_s": {
+                "pcie_h2d_pinned": round(h2d_gbs * 1e3 / fb, 1), "h2d_gbs": round(h2d_gbs, 2),
+                "host_md5_cores_x_rate": round(share * md5_gbs * 1e3 / fb, 1), "cores": share,
+                "one_file_md5_floor_ms": round(md5_s * 1e3, 2)},
+            "path": "pinned host PCM -> flacgpu_encode_file per file (one context + host thread each): H2D, "
+                    "kernels, D2H pipelined in 2048-frame chunks; MD5 on a host thread per file beside the "
+                    "encode; 73-byte header + frames in host memory (pinned)",
             "output_ok": bool(ok)}
 
 
@@ -682,6 +698,11 @@ def main():
             e2e = end_to_end(args)
         if not args.no_cpu:
             cpu = cpu_baseline(buf, args)
+
+    if e2e and cpu:
+        e2e["vs_cpu_measured_P_cores"] = round(e2e["value"] / cpu["value"], 2)
+        if cpu.get("single_socket_estimate"):
+            e2e["vs_cpu_single_socket_estimate"] = round(e2e["value"] / cpu["single_socket_estimate"], 2)
 
     if rank == 0:
         cfg = (args.config or "c2").upper()

@@ -16,10 +16,10 @@
  * Threading: one context per GPU per host thread; a context is not
  * thread-safe.  All functions return FLACGPU_OK (0) or a negative error code.
  *
- * Streams: `void *hip_stream` is a hipStream_t passed through to HIP unchanged,
- * except NULL, which selects the context's own (non-blocking) stream.  The HIP
- * null stream is NOT NULL here: pass FLACGPU_STREAM_LEGACY (== hipStreamLegacy)
- * to order the work against legacy-default-stream work (e.g. a framework whose
+ * Streams: `void *hip_stream` is a hipStream_t, except two values: NULL selects
+ * the context's own (non-blocking) stream, and FLACGPU_STREAM_LEGACY selects the
+ * HIP null stream (legacy default-stream semantics), which orders the work
+ * against default-stream producers and consumers (e.g. a framework whose
  * current stream handle is 0).
  */
 #ifndef FLACGPU_H
@@ -34,7 +34,7 @@ extern "C" {
 
 #define FLACGPU_ABI_VERSION 3
 
-/* the legacy null stream as a hip_stream argument (== hipStreamLegacy) */
+/* the HIP null (legacy default) stream as a hip_stream argument */
 #define FLACGPU_STREAM_LEGACY ((void *)1)
 
 /* Error codes (map to the Zig error set

@@ -297,3 +297,23 @@ def test_default_stream_producer_is_ordered():
     ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, 2, 16, 44100)
     assert got_sizes == ref_sizes and got == ref
     assert flacgpu._stream(0) == flacgpu.STREAM_LEGACY and flacgpu._stream(None) is None
+
+
+@pytest.mark.parametrize("kernel", ["0", "1", "2", "3", "4", "5"])
+def test_md5_kernels_ragged(kernel, monkeypatch):
+    """Every stream-MD5 kernel geometry (FLACGPU_MD5_KERNEL: 0 per-lane loads, 1 the default
+    coalesced LDS-DMA ring, 2..5 ring variants) on 300 streams whose whole-block counts run
+    0..47 with ragged tails (odd and even chunk counts, lanes ending at every ring slot, partial
+    waves and workgroups), 4-byte aligned offsets: digests == hashlib."""
+    monkeypatch.setenv("FLACGPU_MD5_KERNEL", kernel)
+    rng = np.random.Generator(np.random.PCG64(4242))
+    n_streams = 300
+    lengths = [int(x) for x in rng.integers(0, 48 * 16 + 16, size=n_streams)]  # samples (4 B each)
+    lengths[:6] = [0, 1, 16, 32, 47 * 16 + 15, 5000]
+    offs, size = _layout(lengths, 4, (0, 4, 8, 12), gap=12)
+    buf = bytearray(rng.integers(0, 256, size=size, dtype=np.uint8).tobytes())
+    with _encoder(2, 16, 44100, max_frames=512) as enc:
+        res, _ = _run_plan(enc, bytes(buf), offs, lengths, md5="join")
+    for s, (_, _, dig) in enumerate(res):
+        want = hashlib.md5(bytes(buf[offs[s]:offs[s] + 4 * lengths[s]])).digest()
+        assert dig == want, f"stream {s} ({lengths[s]} samples): MD5 kernel {kernel}"

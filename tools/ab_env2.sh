@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B of env knobs on a bench line, alternating.  Usage: tools/ab_env2.sh <tag> "<VAR=val ...>" ...
+set -o pipefail
+TAG=$1; shift
+mkdir -p gpurun_out
+ARGS=${AB_ARGS:-"--steps 20 --warmup 3 --no-cpu --no-curve --no-e2e --no-sharded --verify-streams 8"}
+for rep in 1 2; do
+  i=0
+  for V in "$@"; do
+    i=$((i+1))
+    out=gpurun_out/ab_${TAG}_${i}_$rep.json
+    env $V timeout -k 10 200 python bench.py $ARGS > $out 2> $out.err || { echo "FAIL [$V]"; tail -5 $out.err; exit 1; }
+    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'], d['output_ok'], d['kernel_ms_per_step'])" $out "[$V]"
+  done
+done

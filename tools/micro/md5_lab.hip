@@ -88,6 +88,117 @@ k_md5(const uint8_t *base, uint64_t stride, uint64_t nblocks, uint32_t n, uint32
     out[s] = st[0] ^ st[1] ^ st[2] ^ st[3];
 }
 
+// DATA 3: coalesced LDS-DMA ring.  Two waves per workgroup, 64 streams per wave.  Chunk c of a
+// stream = its blocks 2c, 2c+1 (128 B, one cache line).  LDS-DMA instruction i of a chunk moves
+// 8 streams x 128 B (8 lines instead of 64): lane j -> stream 8i + j/8, LDS slot u = j % 8 of that
+// stream's 128-B row, holding piece p = (u - (stream>>1)) & 7, so that the 16 lanes of a
+// ds_read_b128 quarter hit 16 distinct 16-B bank groups.  R chunks in flight per wave.
+template <int R>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(7, 8)))
+k_md5_lds(const uint8_t *base, uint64_t stride, uint64_t nblocks, uint32_t n, uint32_t *out) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2][R][8192];
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint32_t g0 = blockIdx.x * 128 + w * 64;
+    const uint32_t s = g0 + l;
+    const uint64_t nchunks = nblocks / 2;
+    uint8_t *ring = &lds[w][0][0];
+    auto issue = [&](uint64_t c) {
+        uint8_t *dst = ring + (c % R) * 8192;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t sl = 8 * i + (l >> 3), u = l & 7, p = (u - (sl >> 1)) & 7;
+            const uint8_t *src = base + (uint64_t)(g0 + sl) * stride + 128 * c + 16 * p;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(dst + 1024 * i), 16, 0, 0);
+        }
+    };
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u + s};
+    for (int c = 0; c < R; c++) issue(c);
+    const uint32_t row = 1024 * (l >> 3) + 128 * (l & 7);
+    for (uint64_t c = 0; c < nchunks; c++) {
+        // chunk c landed when at most the R - 1 younger chunks' 8 DMAs each are outstanding
+        if constexpr (R == 3) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else if constexpr (R == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+        const uint8_t *buf = ring + (c % R) * 8192 + row;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            uint32_t m[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t p = 4 * k + q;
+                const v4 v = *(const v4 *)(buf + 16 * ((p + (l >> 1)) & 7));
+                m[4 * q] = v.x; m[4 * q + 1] = v.y; m[4 * q + 2] = v.z; m[4 * q + 3] = v.w;
+            }
+            compress(st, m);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(c + R < nchunks ? c + R : nchunks - 1);  // a redundant refill keeps vmcnt counting uniform
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    out[s] = st[0] ^ st[1] ^ st[2] ^ st[3];
+}
+
+// DATA 6/7: the same LDS ring filled by a third, loader-only wave: the two compute waves never
+// issue a DMA (an LDS-DMA instruction costs its issuing wave ~60-180 cycles); per chunk one
+// barrier says "chunk c landed" and one says "chunk c read into registers".
+__device__ __forceinline__ void bar_raw() { asm volatile("s_barrier" ::: "memory"); }
+template <int R>
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(7, 8)))
+k_md5_ldr(const uint8_t *base, uint64_t stride, uint64_t nblocks, uint32_t n, uint32_t *out) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[R][2][8192];
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint64_t nchunks = nblocks / 2;
+    if (w == 2) {
+        auto issue = [&](uint64_t c) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                uint8_t *dst = &lds[c % R][h][0];
+                const uint32_t g0 = blockIdx.x * 128 + h * 64;
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const uint32_t sl = 8 * i + (l >> 3), u = l & 7, p = (u - (sl >> 1)) & 7;
+                    const uint8_t *src = base + (uint64_t)(g0 + sl) * stride + 128 * c + 16 * p;
+                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,
+                                                     (__attribute__((address_space(3))) void *)(dst + 1024 * i), 16, 0, 0);
+                }
+            }
+        };
+        for (int c = 0; c < R; c++) issue(c);
+        for (uint64_t c = 0; c < nchunks; c++) {
+            if constexpr (R == 3) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+            else if constexpr (R == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+            bar_raw();  // A: chunk c landed
+            bar_raw();  // B: chunk c read
+            issue(c + R < nchunks ? c + R : nchunks - 1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
+    const uint32_t s = blockIdx.x * 128 + w * 64 + l;
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u + s};
+    const uint32_t row = 1024 * (l >> 3) + 128 * (l & 7);
+    for (uint64_t c = 0; c < nchunks; c++) {
+        bar_raw();  // A
+        const uint8_t *buf = &lds[c % R][w][0] + row;
+        uint32_t m[2][16];
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t p = 4 * k + q;
+                const v4 v = *(const v4 *)(buf + 16 * ((p + (l >> 1)) & 7));
+                m[k][4 * q] = v.x; m[k][4 * q + 1] = v.y; m[k][4 * q + 2] = v.z; m[k][4 * q + 3] = v.w;
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar_raw();  // B
+        compress(st, m[0]);
+        compress(st, m[1]);
+    }
+    out[s] = st[0] ^ st[1] ^ st[2] ^ st[3];
+}
+
 // ---- hogs -------------------------------------------------------------------------------------
 #define OP4(i) asm volatile("v_add3_u32 %0, %0, %1, 3\n v_xad_u32 %1, %1, %2, %0\n v_bitop3_b32 %2, %2, %3, %0 bitop3:0xe4\n v_alignbit_b32 %3, %3, %2, 7" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
 #define OP16(i) OP4(i##0) OP4(i##1) OP4(i##2) OP4(i##3)
@@ -165,6 +276,11 @@ int main(int argc, char **argv) {
         if (data == 0) hipLaunchKernelGGL(k_md5<0>, g, b, 0, sa, d, stride, nblocks, n, o);
         if (data == 1) hipLaunchKernelGGL(k_md5<1>, g, b, 0, sa, d, stride, nblocks, n, o);
         if (data == 2) hipLaunchKernelGGL(k_md5<2>, g, b, 0, sa, d, stride, nblocks, n, o);
+        if (data == 3) hipLaunchKernelGGL(k_md5_lds<2>, dim3(n / 128), dim3(128), 0, sa, d, stride, nblocks, n, o);
+        if (data == 4) hipLaunchKernelGGL(k_md5_lds<3>, dim3(n / 128), dim3(128), 0, sa, d, stride, nblocks, n, o);
+        if (data == 5) hipLaunchKernelGGL(k_md5_lds<4>, dim3(n / 128), dim3(128), 0, sa, d, stride, nblocks, n, o);
+        if (data == 6) hipLaunchKernelGGL(k_md5_ldr<3>, dim3(n / 128), dim3(192), 0, sa, d, stride, nblocks, n, o);
+        if (data == 7) hipLaunchKernelGGL(k_md5_ldr<4>, dim3(n / 128), dim3(192), 0, sa, d, stride, nblocks, n, o);
     };
     auto hog = [&](int h) {
         if (h == 1) hipLaunchKernelGGL(k_valu<0>, dim3(hog_wgs), dim3(256), 0, sb, o + (8u << 20), small_iters);
@@ -174,7 +290,7 @@ int main(int argc, char **argv) {
             hipLaunchKernelGGL(k_mem, dim3(cus * 4), dim3(256), 0, sb, d, pieces, o + (8u << 20), tk);
         }
     };
-    const char *dn[3] = {"hbm", "cached", "noload"}, *hn[4] = {"alone", "valu_small", "valu_big", "mem"};
+    const char *dn[8] = {"hbm", "cached", "noload", "lds_r2", "lds_r3", "lds_r4", "ldr_r3", "ldr_r4"}, *hn[4] = {"alone", "valu_small", "valu_big", "mem"};
     float hog_alone[4] = {0, 0, 0, 0};
     for (int h = 1; h < 4; h++) {
         for (int r = 0; r < 3; r++) {
@@ -183,7 +299,8 @@ int main(int argc, char **argv) {
         }
         printf("hog %-10s alone %.3f ms\n", hn[h], hog_alone[h]);
     }
-    for (int data = 0; data < 3; data++) {
+    for (int data = 0; data < 8; data++) {
+        if (data == 1 || data == 2 || data == 3) continue;
         for (int h = 0; h < 4; h++) {
             float ma = 0, hb = 0;
             for (int r = 0; r < 3; r++) {

@@ -27,7 +27,7 @@ hipError_t launch_frame_totals(const EncodeArgs &a, hipStream_t st);
 hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, uint64_t *part,
                        hipStream_t st);
 hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *fin,
-                              uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st);
+                              uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st, int kernel, int prio);
 hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipStream_t st);
 hipError_t launch_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks, hipStream_t st);
 hipError_t launch_streaminfo_replay(const uint32_t *sizes, uint64_t n, uint32_t *minmax, hipStream_t st);
@@ -109,6 +109,8 @@ struct flacgpu_ctx {
     // streaming MD5 (one stream): a host core by default (FLACGPU_MD5_HOST), or one GPU
     // lane fed by bounded chunks (FLACGPU_MD5_DEVICE, opt-in)
     int md5_engine = FLACGPU_MD5_HOST;
+    int md5_kernel = 1;  // batched stream MD5: 1 = coalesced LDS-DMA ring, 0 = per-lane loads (A/B knob)
+    int md5_prio = 0;    // issue priority of the MD5 waves beside the encode (A/B knob)
     HostMd5 host_md5;
     uint32_t *d_md5_state = nullptr;
     uint32_t *d_md5_blocks = nullptr;
@@ -188,6 +190,14 @@ int hip_err(hipError_t e) { return e == hipSuccess ? FLACGPU_OK : (e == hipError
         hipError_t e_ = (x);                    \
         if (e_ != hipSuccess) return hip_err(e_); \
     } while (0)
+
+// The C ABI's hip_stream: NULL = the context's own stream, FLACGPU_STREAM_LEGACY = the HIP null
+// stream (legacy default-stream semantics: the handle-0 stream of a framework), else a hipStream_t.
+static hipStream_t pick_stream(const flacgpu_ctx *c, void *hip_stream) {
+    if (!hip_stream) return c->stream;
+    if (hip_stream == FLACGPU_STREAM_LEGACY) return (hipStream_t)0;
+    return (hipStream_t)hip_stream;
+}
 
 int validate(const flacgpu_config *cfg) {
     if (!cfg) return FLACGPU_ERR_INVALID_INPUT;
@@ -455,6 +465,9 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     const uint32_t pack_wgs = c->B == 4 ? 2u : 4u;
     c->pack_dbuf = pack_layout(c->C, c->B, c->image_bytes, true).total * pack_wgs <= 160u * 1024u;
     if (const char *e = std::getenv("FLACGPU_PACK_DBUF")) c->pack_dbuf = c->pack_dbuf && e[0] == '1';  // tuning knob
+    if (const char *e = std::getenv("FLACGPU_MD5_KERNEL")) c->md5_kernel = std::atoi(e);  // A/B knob
+    if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);      // A/B knob
+    if (const char *e = std::getenv("FLACGPU_MD5_DIAG")) c->md5_prio |= std::atoi(e) << 8;  // diagnostics
     c->lds_pack = pack_layout(c->C, c->B, c->image_bytes, c->pack_dbuf).total;
     // CRC fold: half-segments of H words (odd), H <= ceil(image words / (2 * pack threads))
     c->crc_hmax = ((c->image_bytes / 4u + 2u * c->nt_pack - 1u) / (2u * c->nt_pack)) | 1u;
@@ -945,7 +958,7 @@ int flacgpu_plan_advance(flacgpu_plan *p, uint64_t frames, void *hip_stream) {
     if (frames > (1ull << 36) - 1 - p->max_number) return FLACGPU_ERR_INVALID_INPUT;  // u36 frame numbers
     flacgpu_ctx *c = p->ctx;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t st = pick_stream(c, hip_stream);
     HIPCHK(launch_advance_jobs(p->d_jobs, p->n_frames, frames, st));
     p->max_number += frames;
     return FLACGPU_OK;
@@ -960,13 +973,13 @@ int flacgpu_encode_plan_device_ex(flacgpu_ctx *c, const flacgpu_plan *p, const v
     // a stream that continues past this segment has no digest yet: its state must be carried
     if (p->d_md5_fin && d_md5 && !d_md5_state) return FLACGPU_ERR_INVALID_INPUT;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t st = pick_stream(c, hip_stream);
     if (c->records_on && p->n_frames > c->max_frames) return FLACGPU_ERR_INVALID_INPUT;
     uint8_t *desc = p->d_desc ? p->d_desc : c->d_desc;
     // MD5 of every stream on a second stream, overlapping the encode kernels (joined back into
     // st unless the caller owns the MD5 stream)
     const bool join = md5_stream == nullptr;
-    hipStream_t ms = join ? c->aux : (hipStream_t)md5_stream;
+    hipStream_t ms = join ? c->aux : pick_stream(c, md5_stream);
     const bool md5 = (d_md5 || d_md5_state) && p->n_streams;
     if (md5) {
         hipEvent_t fork = join ? c->fork : get_event(c);
@@ -977,7 +990,7 @@ int flacgpu_encode_plan_device_ex(flacgpu_ctx *c, const flacgpu_plan *p, const v
         {
             Timed t(c, FLACGPU_K_MD5, ms);
             HIPCHK(launch_md5_streams((const uint8_t *)d_pcm, p->d_md5_offs, p->d_md5_lens, p->d_md5_fin, p->n_streams,
-                                      (Md5State *)d_md5_state, d_md5, ms));
+                                      (Md5State *)d_md5_state, d_md5, ms, c->md5_kernel, c->md5_prio));
         }
         if (join) HIPCHK(hipEventRecord(c->join, ms));
     }
@@ -1006,7 +1019,7 @@ int flacgpu_streaminfo_replay_device(flacgpu_ctx *c, const uint32_t *d_frame_byt
                                      uint32_t *d_minmax, void *hip_stream) {
     if (!c || !d_minmax || (n_frames && !d_frame_bytes)) return FLACGPU_ERR_INVALID_INPUT;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t st = pick_stream(c, hip_stream);
     HIPCHK(launch_streaminfo_replay(d_frame_bytes, n_frames, d_minmax, st));
     return FLACGPU_OK;
 }
@@ -1014,7 +1027,7 @@ int flacgpu_streaminfo_replay_device(flacgpu_ctx *c, const uint32_t *d_frame_byt
 int flacgpu_sync_check(flacgpu_ctx *c, void *hip_stream) {
     if (!c) return FLACGPU_ERR_INVALID_INPUT;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(hip_stream ? (hipStream_t)hip_stream : c->stream));
+    HIPCHK(hipStreamSynchronize(pick_stream(c, hip_stream)));
     return check_device_error(c);
 }
 

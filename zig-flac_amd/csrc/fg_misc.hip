@@ -352,7 +352,7 @@ __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16
 // shares on the same CU, 4x less busy.
 typedef uint32_t md5_v4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FG_MD5_AHEAD
-#define FG_MD5_AHEAD 1
+#define FG_MD5_AHEAD 2
 #endif
 // waves per SIMD the MD5 kernel is compiled for: at 7 it fits 72 VGPRs (one message block in flight ahead), so its waves take
 // little of the register file the encode kernels running beside it occupy
@@ -360,6 +360,9 @@ typedef uint32_t md5_v4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FG_MD5_WPE 7
 #endif
 constexpr int kMd5Ahead = FG_MD5_AHEAD;
+#ifndef FG_MD5_PRIO
+#define FG_MD5_PRIO 0
+#endif
 // Streams per MD5 workgroup.  The encode kernels fill their SIMDs' register files (k_analyze
 // 4 x 128 VGPRs, k_pack4 8 x 64), so a SIMD that holds an MD5 wave loses one encode wave and its
 // CU one encode workgroup.  Four MD5 waves per workgroup (one per SIMD of one CU) confine that
@@ -391,9 +394,6 @@ __global__ void __launch_bounds__(kMd5Wg) __attribute__((amdgpu_waves_per_eu(FG_
     // issue priority 3 they win every arbitration and the encode waves beside them lose issue
     // slots; at the default 0 the encode runs ~5-10 % faster with 16384 streams while each MD5
     // chain slows only slightly (tools/ab_md5.sh A/B).
-#ifndef FG_MD5_PRIO
-#define FG_MD5_PRIO 0
-#endif
     __builtin_amdgcn_s_setprio(FG_MD5_PRIO);
     const uint8_t *p = base + offs[s];
     const uint64_t len = lens[s];
@@ -418,22 +418,32 @@ __global__ void __launch_bounds__(kMd5Wg) __attribute__((amdgpu_waves_per_eu(FG_
         }
     }
     const uint64_t full = len >> 6;
-    // ring of kMd5Ahead + 1 message blocks: block b is consumed while b + 1 .. b + kMd5Ahead load
-    uint32_t m[kMd5Ahead + 1][16];
+    // Ring of R = kMd5Ahead + 1 message blocks in registers: block b is compressed while blocks
+    // b + 1 .. b + kMd5Ahead are in flight.  The loads inside the loop are UNCONDITIONAL (the
+    // block index is clamped to the lane's last block, a harmless re-read): a load under a
+    // per-lane condition makes the compiler merge "loaded" and "old" ring values at the join,
+    // i.e. copy the whole ring through v_mov behind an s_waitcnt vmcnt(0) -- which waited for
+    // the blocks just issued and exposed one full memory latency per loop trip (beside the
+    // encode kernels' traffic, ~1 us per 64-B block; tools/micro/md5_lab.hip).
+    constexpr int R = kMd5Ahead + 1;
+    uint32_t m[R][16];
+    const uint64_t last = full ? full - 1 : 0;
+    if (full)
 #pragma unroll
-    for (int k = 0; k < kMd5Ahead + 1; k++)
-        if ((uint64_t)k < full) md5_load_block(p + 64u * k, m[k]);
+        for (int k = 0; k < R; k++) md5_load_block(p + 64u * min((uint64_t)k, last), m[k]);
     uint64_t b = 0;
-    for (; b + kMd5Ahead + 1 <= full; b += kMd5Ahead + 1) {
+    for (; b + R <= full; b += R) {
 #pragma unroll
-        for (int k = 0; k < kMd5Ahead + 1; k++) {
+        for (int k = 0; k < R; k++) {
             md5_compress(st, m[k]);
-            const uint64_t nb = b + k + kMd5Ahead + 1;
-            if (nb < full) md5_load_block(p + 64u * nb, m[k]);
+            md5_load_block(p + 64u * min(b + k + R, last), m[k]);
+            // keep the refill here, R - 1 compressions ahead of its use: without a fence the
+            // scheduler sinks every refill to the end of the trip (prefetch distance ~0)
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 #pragma unroll
-    for (int k = 0; k < kMd5Ahead; k++)
+    for (int k = 0; k < R - 1; k++)
         if (b + k < full) md5_compress(st, m[k]);
     if (fin) {
         // tail + padding (one or two blocks): the rem < 64 tail bytes as dwords (the dword holding
@@ -450,6 +460,195 @@ __global__ void __launch_bounds__(kMd5Wg) __attribute__((amdgpu_waves_per_eu(FG_
             if ((uint32_t)i < wr) {
                 v = tp32[i];
             } else if ((uint32_t)i == wr) {
+                for (uint32_t q = 0; q < br; q++) v |= (uint32_t)tp[4u * i + q] << (8u * q);
+                v |= 0x80u << (8u * br);
+            }
+            mt[i] = v;
+        }
+        const uint64_t bits = (done + len) * 8;
+        if (rem < 56) {
+            mt[14] = (uint32_t)bits;
+            mt[15] = (uint32_t)(bits >> 32);
+            md5_compress(st, mt);
+        } else {
+            md5_compress(st, mt);
+#pragma unroll
+            for (int i = 0; i < 14; i++) mt[i] = 0;
+            mt[14] = (uint32_t)bits;
+            mt[15] = (uint32_t)(bits >> 32);
+            md5_compress(st, mt);
+        }
+        if (digests)
+            for (int i = 0; i < 4; i++)
+                for (int j = 0; j < 4; j++) digests[16 * s + 4 * i + j] = (uint8_t)(st[i] >> (8 * j));
+    }
+    if (states) {
+        Md5State o;
+        o.h[0] = st[0];
+        o.h[1] = st[1];
+        o.h[2] = st[2];
+        o.h[3] = st[3];
+        o.bytes = done + len;
+        o.flags = fin ? 1u : 0u;
+        o.pad = 0;
+        states[s] = o;
+    }
+}
+
+// ------------------------------------------------------------------------
+// The same MD5 with COALESCED message loads through an LDS ring (the default).
+//
+// k_md5_streams above loads each lane's own 16-B pieces: one dwordx4 touches 64 cache lines
+// 64 KiB apart.  Beside the encode kernels' LDS-DMA staging on the same CUs those loads queue
+// in the texture path, and a block's load latency, not the 64-step chain, sets the rate
+// (tools/micro/md5_lab.hip: 1.86 us per block beside an LDS-DMA streamer, 1.2 alone, against
+// 0.5 with no loads at all).  Here the blocks arrive by LDS-DMA in whole cache lines: chunk c of
+// a stream is its blocks CB c .. CB c + CB - 1; DMA instruction i of a chunk moves 16 / CB
+// streams' chunks (64 CB bytes each, one line for CB = 2) into LDS rows of 64 CB bytes, the
+// 16-B pieces of a row rotated by the stream index so that the 16 lanes of a ds_read_b128
+// quarter read 16 distinct bank groups.  R chunks are in flight per wave; the wave waits for
+// chunk c with vmcnt(4 CB (R - 1)) and re-fills its slot once the chunk is in registers.  All
+// lanes take part in every DMA (a lane fetches OTHER streams' pieces), so the chunk loop is
+// wave-uniform and a lane whose segment has ended only skips the compression.
+// ------------------------------------------------------------------------
+// chunk of CB blocks (1 or 2), R chunks in flight per wave, NWV waves (64 streams each) per workgroup
+template <uint32_t CB> struct Md5Geo {
+    static constexpr uint32_t Chunk = 4096u * CB;  // LDS bytes per chunk per wave (64 streams)
+    static constexpr uint32_t Per = 16u / CB;      // streams per DMA instruction
+    static constexpr uint32_t Pcs = 4u * CB;       // 16-B pieces per stream chunk = DMAs per chunk
+};
+
+// rotation of stream sl's row: the lanes of a 16-lane quarter (consecutive sl) that share a
+// 256-B bank window get distinct 16-B slots
+template <uint32_t CB>
+__device__ __forceinline__ uint32_t md5_rot(uint32_t sl) { return CB == 2 ? (sl >> 1) : (sl >> 2); }
+
+template <uint32_t CB, uint32_t R, uint32_t NWV>
+__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(4, 8)))
+k_md5_streams_lds(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *final_flags,
+                  uint32_t n_streams, Md5State *states, uint8_t *digests, const uint8_t *dummy, uint32_t prio,
+                  uint32_t diag) {
+    constexpr uint32_t kMd5CB = CB, kMd5R = R;
+    constexpr uint32_t kMd5Chunk = Md5Geo<CB>::Chunk, kMd5Per = Md5Geo<CB>::Per, kMd5Pcs = Md5Geo<CB>::Pcs;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[NWV][R][kMd5Chunk];
+    const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (prio) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(0);
+    const bool live = s < n_streams;
+    const uint8_t *p = dummy;
+    uint64_t len = 0, done = 0;
+    bool fin = false;
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (live) {
+        p = base + offs[s];
+        len = lens[s];
+        fin = final_flags ? final_flags[s] != 0 : true;
+        if (states) {
+            const Md5State in = states[s];
+            st[0] = in.h[0];
+            st[1] = in.h[1];
+            st[2] = in.h[2];
+            st[3] = in.h[3];
+            done = in.bytes;
+            if (in.flags & 1u) {
+                // already finalised (Md5.final ran, encoder.zig:168-170): h IS the digest; the
+                // state stays as it is and a requested digest is the finished one
+                if (fin && digests)
+                    for (int i = 0; i < 4; i++)
+                        for (int j = 0; j < 4; j++) digests[16 * s + 4 * i + j] = (uint8_t)(st[i] >> (8 * j));
+                len = 0;
+                fin = false;
+                states = nullptr;  // nothing to store back for this lane
+            }
+        }
+    }
+    const uint64_t full = len >> 6;
+    if (!full) p = dummy;  // a lane with no whole block serves its DMA pieces from a valid address
+    // the pointer / whole-block count of the stream each of this lane's DMA pieces belongs to
+    const uint8_t *src_p[kMd5Pcs];
+    uint64_t src_full[kMd5Pcs];
+    uint32_t src_rot[kMd5Pcs];
+#pragma unroll
+    for (uint32_t i = 0; i < kMd5Pcs; i++) {
+        const uint32_t sl = kMd5Per * i + l / kMd5Pcs;
+        src_p[i] = (const uint8_t *)__shfl((unsigned long long)(uintptr_t)p, (int)sl);
+        src_full[i] = __shfl((unsigned long long)full, (int)sl);
+        src_rot[i] = ((l % kMd5Pcs) - md5_rot<CB>(sl)) % kMd5Pcs;  // piece index this lane moves
+    }
+    // wave-uniform chunk count
+    uint64_t wmax = full;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) wmax = max(wmax, (uint64_t)__shfl_xor((unsigned long long)wmax, d));
+    const uint64_t nch = (wmax + kMd5CB - 1) / kMd5CB;
+    uint8_t *wr = &ring[wave][0][0];
+    // chunk c into ring slot `slot` (normally c % R)
+    auto issue = [&](uint32_t slot, uint64_t c) {
+        uint8_t *dst = wr + slot * kMd5Chunk;
+#pragma unroll
+        for (uint32_t i = 0; i < kMd5Pcs; i++) {
+            // piece src_rot[i] of chunk c of stream sl; pieces past the stream's whole blocks
+            // re-read its first piece (never compressed)
+            const uint64_t off = 64u * kMd5CB * c + 16u * src_rot[i];
+            const uint8_t *q = src_p[i] + (off + 16u <= 64u * src_full[i] ? off : 0u);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)q,
+                                             (__attribute__((address_space(3))) void *)(dst + 1024u * i), 16, 0, 0);
+        }
+    };
+    // diag (diagnostics only, wrong digests): bit 0 = no LDS reads (message words from registers),
+    // bit 1 = no DMA and no waits
+    const bool dma = !(diag & 2u), rd = !(diag & 1u);
+    if (dma)
+        for (uint32_t c = 0; c < kMd5R; c++) issue(c, c < nch ? c : 0);
+    const uint32_t row = 64u * kMd5CB * l, rot = md5_rot<CB>(l);
+    for (uint64_t c = 0; c < nch; c++) {
+        // chunk c has landed once at most the R - 1 younger chunks' DMAs are outstanding
+        if (!dma) {
+        } else if constexpr (kMd5R * kMd5Pcs == 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if constexpr (kMd5R * kMd5Pcs == 12 && kMd5Pcs == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if constexpr (kMd5R * kMd5Pcs == 16 && kMd5Pcs == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if constexpr (kMd5R * kMd5Pcs == 16 && kMd5Pcs == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else if constexpr (kMd5R * kMd5Pcs == 24) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint8_t *buf = wr + (uint32_t)(c % kMd5R) * kMd5Chunk + row;
+        uint32_t m[kMd5CB][16];
+#pragma unroll
+        for (uint32_t k = 0; k < kMd5CB; k++)
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t pc = 4u * k + q;
+                const md5_v4 v = rd ? *(const md5_v4 *)(buf + 16u * ((pc + rot) % kMd5Pcs))
+                                    : md5_v4{st[0] + pc, st[1], st[2], st[3]};
+                m[k][4 * q] = v.x;
+                m[k][4 * q + 1] = v.y;
+                m[k][4 * q + 2] = v.z;
+                m[k][4 * q + 3] = v.w;
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // the slot is free once its words are in registers: re-fill it with chunk c + R (past the
+        // end: chunk c again, into the same slot -- a redundant DMA that keeps the vmcnt
+        // arithmetic uniform and never lands in a slot that is still to be read)
+        if (dma) issue((uint32_t)(c % kMd5R), c + kMd5R < nch ? c + kMd5R : c);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (uint32_t k = 0; k < kMd5CB; k++)
+            if (kMd5CB * c + k < full) md5_compress(st, m[k]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!live) return;
+    if (fin) {
+        // tail + padding, as in k_md5_streams
+        const uint32_t rem = (uint32_t)(len & 63);
+        const uint8_t *tp = base + offs[s] + full * 64;
+        const uint32_t *tp32 = (const uint32_t *)tp;
+        uint32_t mt[16];
+        const uint32_t wrm = rem >> 2, br = rem & 3u;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            uint32_t v = 0;
+            if ((uint32_t)i < wrm) {
+                v = tp32[i];
+            } else if ((uint32_t)i == wrm) {
                 for (uint32_t q = 0; q < br; q++) v |= (uint32_t)tp[4u * i + q] << (8u * q);
                 v |= 0x80u << (8u * br);
             }
@@ -540,11 +739,34 @@ hipError_t launch_streaminfo_replay(const uint32_t *sizes, uint64_t n, uint32_t 
     return hipGetLastError();
 }
 
+// kernel 0: per-lane loads (k_md5_streams); otherwise the coalesced LDS-DMA ring
+// (k_md5_streams_lds) in geometry `kernel` (1 = the default, 2.. = A/B variants); prio: issue
+// priority of the MD5 waves (0 or 3)
+template <uint32_t CB, uint32_t R, uint32_t NWV>
+static void launch_md5_lds(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *fin,
+                           uint32_t n, Md5State *states, uint8_t *digests, uint32_t prio, uint32_t diag,
+                           hipStream_t st) {
+    const uint8_t *dummy = states ? (const uint8_t *)states : digests;  // >= 16 valid bytes
+    const uint32_t wg = 64u * NWV;
+    hipLaunchKernelGGL((k_md5_streams_lds<CB, R, NWV>), dim3((n + wg - 1) / wg), dim3(wg), 0, st, base, offs, lens, fin, n,
+                       states, digests, dummy, prio, diag);
+}
+
 hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *fin,
-                              uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st) {
+                              uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st, int kernel, int prio) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_md5_streams, dim3((n + kMd5Wg - 1) / kMd5Wg), dim3(kMd5Wg), 0, st, base, offs, lens, fin, n, states,
-                       digests);
+    const uint32_t pr = prio & 1u, dg = (uint32_t)prio >> 8;  // prio bits 8..9: diagnostics
+    switch (kernel) {
+        case 0:
+            hipLaunchKernelGGL(k_md5_streams, dim3((n + kMd5Wg - 1) / kMd5Wg), dim3(kMd5Wg), 0, st, base, offs, lens, fin,
+                               n, states, digests);
+            break;
+        case 2: launch_md5_lds<1, 3, 4>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 48 KiB
+        case 3: launch_md5_lds<2, 3, 2>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 48 KiB
+        case 4: launch_md5_lds<1, 2, 4>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 32 KiB
+        case 5: launch_md5_lds<2, 2, 2>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 32 KiB
+        default: launch_md5_lds<2, 2, 4>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 64 KiB
+    }
     return hipGetLastError();
 }
 

@@ -253,7 +253,7 @@ def exported_symbols() -> list:
     ]
 
 
-STREAM_LEGACY = 1  # FLACGPU_STREAM_LEGACY == hipStreamLegacy
+STREAM_LEGACY = 1  # FLACGPU_STREAM_LEGACY: the library maps it to the HIP null stream
 
 
 def _stream(h: Optional[int]) -> Optional[int]:
