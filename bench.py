@@ -84,7 +84,7 @@ def parse():
     p.add_argument("--no-md5", action="store_true", help="skip the per-stream GPU MD5 (diagnostics only)")
     p.add_argument("--verify-streams", type=int, default=64, help="streams compared with the oracle after timing")
     p.add_argument("--no-curve", action="store_true")
-    p.add_argument("--curve", default="8,64,1024,8192,16384")
+    p.add_argument("--curve", default="8,64,1024,8192,16384,32768,65536")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-files", default="8,16,32", help="file counts of the end-to-end curve")
     p.add_argument("--e2e-minutes", type=float, default=10.0)

@@ -9,8 +9,8 @@ set -e
 TAG=${1:-r2}; shift || true
 CFG=${1:-c2}; shift || true
 FRAMES=${1:-65536}; shift || true
-STREAMS=${1:-8192}; shift || true
-ARGS="--config $CFG --frames $FRAMES --streams $STREAMS --steps 5 --warmup 2 --no-cpu --no-curve --no-e2e --verify-streams 4 $@"
+STREAMS=${1:-16384}; shift || true
+ARGS="--config $CFG --frames $FRAMES --streams $STREAMS --steps 5 --warmup 2 --no-cpu --no-curve --no-e2e --no-sharded --verify-streams 4 $@"
 REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p $OUT

@@ -30,6 +30,7 @@ hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const u
                               uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st, int kernel, int prio);
 hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipStream_t st);
 hipError_t launch_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks, hipStream_t st);
+uint32_t md5_workgroups(uint32_t n, int kernel);
 hipError_t launch_streaminfo_replay(const uint32_t *sizes, uint64_t n, uint32_t *minmax, hipStream_t st);
 }  // namespace fg
 
@@ -111,6 +112,9 @@ struct flacgpu_ctx {
     int md5_engine = FLACGPU_MD5_HOST;
     int md5_kernel = 1;  // batched stream MD5: 1 = coalesced LDS-DMA ring, 0 = per-lane loads (A/B knob)
     int md5_prio = 0;    // issue priority of the MD5 waves beside the encode (A/B knob)
+    int md5_reserve = -1;  // 1: the analysis grid leaves one workgroup slot per stream-MD5 workgroup
+                           //    queued beside it, 2: the pack grid too, 0: none, -1: auto (A/B knob)
+    uint32_t grid_reserve = 0;  // per call: slots the next analysis / pack launches leave free
     HostMd5 host_md5;
     uint32_t *d_md5_state = nullptr;
     uint32_t *d_md5_blocks = nullptr;
@@ -130,6 +134,7 @@ struct flacgpu_plan {
     FrameJob *d_jobs = nullptr;  // full jobs first, then tail jobs
     uint64_t *d_md5_offs = nullptr, *d_md5_lens = nullptr;
     uint8_t *d_md5_fin = nullptr;  // per-stream final-segment flags (NULL: all final)
+    uint64_t md5_max_len = 0;      // longest stream segment (bytes): the MD5 chain of one call
     uint64_t max_number = 0;       // largest frame number in the table (u36 check on advance)
     std::vector<uint64_t> first_frame;
     uint64_t out_bound = 0;
@@ -262,6 +267,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
         Timed t(c, FLACGPU_K_ANALYZE, st);
         a.jobs = d_jobs;
         a.n_jobs = (uint32_t)n_full;
+        a.grid_reserve = c->grid_reserve;
         if (c->ana_split) {
             a.channels = c->C / 2u;
             a.ch_split = 1;
@@ -272,6 +278,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
         } else {
             HIPCHK(launch_stage(0, a, true, c->nt, c->lds, st));
         }
+        a.grid_reserve = 0;
     }
     if (n_tail) {
         Timed t(c, FLACGPU_K_ANALYZE_TAIL, st);
@@ -297,8 +304,10 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
         if (n_full) {
             a.jobs = d_jobs;
             a.n_jobs = (uint32_t)n_full;
+            a.grid_reserve = c->md5_reserve == 2 ? c->grid_reserve : 0u;
             if (c->nt_pack4) HIPCHK(launch_stage(1, a, true, c->nt_pack4, c->lds_pack4, st));
             else HIPCHK(launch_stage(1, a, true, c->nt_pack, c->lds_pack, st));
+            a.grid_reserve = 0;
         }
         if (n_tail) {
             a.jobs = d_jobs + n_full;
@@ -467,6 +476,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (const char *e = std::getenv("FLACGPU_PACK_DBUF")) c->pack_dbuf = c->pack_dbuf && e[0] == '1';  // tuning knob
     if (const char *e = std::getenv("FLACGPU_MD5_KERNEL")) c->md5_kernel = std::atoi(e);  // A/B knob
     if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);      // A/B knob
+    if (const char *e = std::getenv("FLACGPU_MD5_RESERVE")) c->md5_reserve = std::atoi(e);  // A/B knob
     if (const char *e = std::getenv("FLACGPU_MD5_DIAG")) c->md5_prio |= std::atoi(e) << 8;  // diagnostics
     c->lds_pack = pack_layout(c->C, c->B, c->image_bytes, c->pack_dbuf).total;
     // CRC fold: half-segments of H words (odd), H <= ceil(image words / (2 * pack threads))
@@ -884,6 +894,7 @@ int flacgpu_plan_create_segments(flacgpu_ctx *c, uint32_t n_streams, const uint6
         for (uint32_t s = 0; s < n_streams; s++) {
             p->first_frame[s] = slot;
             lens[s] = samples[s] * fbytes_in;
+            p->md5_max_len = std::max(p->md5_max_len, lens[s]);
             const uint64_t nf = frames_for(samples[s], bs);
             const uint64_t f0 = first_frame_numbers ? first_frame_numbers[s] : 0;
             for (uint64_t f = 0; f < nf; f++, slot++) {
@@ -994,8 +1005,15 @@ int flacgpu_encode_plan_device_ex(flacgpu_ctx *c, const flacgpu_plan *p, const v
         }
         if (join) HIPCHK(hipEventRecord(c->join, ms));
     }
+    // the MD5 workgroups were queued first: the encode kernels' persistent grids leave their slots
+    // auto: only for long chains (>= 4096 blocks per stream per call, e.g. c4's 4 x 96-KiB frames).  A
+    // persistent grid cannot grow back, so the reserved slots idle once the MD5 is done; a shorter
+    // chain started late (after the analysis) still ends before the pack
+    const bool reserve = c->md5_reserve > 0 || (c->md5_reserve < 0 && p->md5_max_len >= (256u << 10));
+    c->grid_reserve = (md5 && reserve) ? md5_workgroups(p->n_streams, c->md5_kernel) : 0u;
     int rc = encode_core(c, (const uint8_t *)d_pcm, p->d_jobs, p->n_full, p->n_tail, desc, d_frame_bytes, d_out,
                          out_cap, d_frame_offsets, d_total, st);
+    c->grid_reserve = 0;
     if (rc) return rc;
     if (join && md5) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
     return FLACGPU_OK;

@@ -132,6 +132,8 @@ struct EncodeArgs {
     unsigned long long *stamps; // diagnostic builds (-DFG_STAMPS): per-phase clock sums
     uint32_t ch_split;          // full-frame analysis: 1 = one workgroup per channel half (channels
                                 // = the half's count), frame totals by k_frame_totals
+    uint32_t grid_reserve;      // host side: persistent workgroups left unlaunched (room for the
+                                // stream-MD5 workgroups queued beside this kernel)
 };
 
 }  // namespace fg

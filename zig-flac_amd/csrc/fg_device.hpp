@@ -2403,7 +2403,10 @@ static hipError_t launch_persistent(KernelT k, const EncodeArgs &a, uint32_t thr
         if (n_cache < 64) cache[n_cache++] = {(const void *)k, threads, lds, dev, resident, cus};
     }
     uint64_t grid = (uint64_t)a.n_jobs << (a.ch_split ? 1 : 0);  // work items (channel halves: two per frame)
-    const uint64_t cap = (uint64_t)resident * (uint64_t)(cus > 0 ? cus : 256);
+    uint64_t cap = (uint64_t)resident * (uint64_t)(cus > 0 ? cus : 256);
+    // leave room for workgroups of a kernel running beside this one (the stream MD5): without it
+    // the persistent grid takes every slot and the other kernel waits for this one to finish
+    if (a.grid_reserve && cap > 4u * (uint64_t)a.grid_reserve) cap -= a.grid_reserve;
     if (grid > cap) grid = cap;
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(k, dim3((uint32_t)grid), dim3(threads), lds, st, a);

@@ -763,11 +763,19 @@ hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const u
             break;
         case 2: launch_md5_lds<1, 3, 4>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 48 KiB
         case 3: launch_md5_lds<2, 3, 2>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 48 KiB
-        case 4: launch_md5_lds<1, 2, 4>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 32 KiB
+        case 4: launch_md5_lds<2, 2, 4>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 64 KiB
         case 5: launch_md5_lds<2, 2, 2>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 32 KiB
-        default: launch_md5_lds<2, 2, 4>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;  // 64 KiB
+        // default: one-block chunks, two in flight, four waves = 32 KiB of LDS, one workgroup in the
+        // footprint of one k_analyze workgroup (37 KiB, 4 x 128 VGPRs)
+        default: launch_md5_lds<1, 2, 4>(base, offs, lens, fin, n, states, digests, pr, dg, st); break;
     }
     return hipGetLastError();
+}
+
+// workgroups a launch_md5_streams(kernel) of n streams occupies
+uint32_t md5_workgroups(uint32_t n, int kernel) {
+    const uint32_t wg = (kernel == 3 || kernel == 5) ? 128u : 256u;
+    return (n + wg - 1u) / wg;
 }
 
 hipError_t launch_md5_blocks(uint32_t *state, const uint32_t *blocks, uint64_t n_blocks, hipStream_t st) {
