@@ -619,6 +619,11 @@ def cpu_baseline(buf, args):
 
 # ---------------------------------------------------------------------------------------------
 def main():
+    # the contract is ONE JSON line on stdout: libraries that print banners there (RCCL prints
+    # its version at communicator init, on every rank) are moved to stderr at the fd level
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     args = parse()
     import numpy as np
     import torch
@@ -759,7 +764,8 @@ def main():
             "end_to_end": e2e,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line))
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     enc.close()
     if dist:
         dist.destroy_process_group()
