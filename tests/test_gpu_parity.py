@@ -208,6 +208,28 @@ def test_pack4_matches_general_pack(monkeypatch, stereo):
     assert outs[0][0] == ref, _diff_msg(outs[0][0], ref)
 
 
+@pytest.mark.parametrize("ch,bits,rate", [(8, 24, 96000), (8, 16, 44100), (6, 32, 96000), (8, 32, 192000)])
+def test_pack_split_matches_whole_frame(monkeypatch, ch, bits, rate):
+    """Frames analysed in channel halves are also packed in channel halves (k_packw split mode:
+    two workgroups per frame, CRC-16 joined as CRC(img0) z^(8 (Lb - e0)) ^ CRC(img1), the byte
+    both halves share merged by the second to arrive); the whole-frame k_packw
+    (FLACGPU_PACK_SPLIT=0) and the restatement must see the same bytes -- including the
+    special blocks (all-zero, full-scale noise: the shared byte at every bit offset) and a tail."""
+    import flacgpu
+
+    n = 4096 * 40 + 333
+    pcm = synth.synth_pcm(n, ch, bits, rate, stream=9)
+    outs = []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("FLACGPU_PACK_SPLIT", knob)
+        with flacgpu.Encoder(ch, bits, rate, max_frames=24) as enc:
+            outs.append(enc.encode_frames(pcm))
+    assert outs[0][1] == outs[1][1], "frame sizes differ between the split and whole-frame pack"
+    assert outs[0][0] == outs[1][0], _diff_msg(outs[0][0], outs[1][0])
+    ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, ch, bits, rate)
+    assert outs[0][1] == ref_sizes and outs[0][0] == ref, _diff_msg(outs[0][0], ref)
+
+
 @pytest.mark.parametrize("cfg,max_frames,n", [
     ((2, 16, 44100), 8, 4096 * 37 + 1001),   # 4-frame chunks: 10 chunks, both halves reused 5x, a tail
     ((2, 24, 96000), 6, 4096 * 13),          # 3-frame chunks, no tail

@@ -98,6 +98,10 @@ struct flacgpu_ctx {
     unsigned long long *d_stamps = nullptr;
     bool records_on = false;
     bool ana_split = false;  // full-frame analysis in channel halves (fg_device.hpp k_analyze)
+    bool pack_split = false;  // full-frame pack in channel halves (fg_packw.hpp k_packw<..., true>)
+    uint32_t nt_psplit = 0, lds_psplit = 0, image_split = 0, crc_hmaxs = 0;
+    uint16_t *d_crc_pows = nullptr;  // CRC fold shifts for the split pack's thread count
+    uint16_t *d_crc_x8 = nullptr;    // z^(8 * 2^i) mod P, i < 24
     uint32_t nt_split = 0, lds_split = 0;
     uint64_t *d_scan_part = nullptr;  // per-4096-frame block sums of the multi-workgroup scan
     uint32_t scan_part_cap = 0;
@@ -263,6 +267,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.crc_hmax = c->crc_hmax;
     a.records = c->records_on ? c->d_records : nullptr;
     a.stamps = c->d_stamps;
+    a.crc_x8 = c->d_crc_x8;
     if (n_full) {
         Timed t(c, FLACGPU_K_ANALYZE, st);
         a.jobs = d_jobs;
@@ -305,8 +310,19 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
             a.jobs = d_jobs;
             a.n_jobs = (uint32_t)n_full;
             a.grid_reserve = c->md5_reserve == 2 ? c->grid_reserve : 0u;
-            if (c->nt_pack4) HIPCHK(launch_stage(1, a, true, c->nt_pack4, c->lds_pack4, st));
-            else HIPCHK(launch_stage(1, a, true, c->nt_pack, c->lds_pack, st));
+            if (c->pack_split) {
+                EncodeArgs h = a;
+                h.channels = c->C / 2u;
+                h.ch_split = 1;
+                h.image_bytes = c->image_split;
+                h.crc_pow4 = c->d_crc_pows;
+                h.crc_hmax4 = c->crc_hmaxs;
+                HIPCHK(launch_stage(1, h, true, c->nt_psplit, c->lds_psplit, st));
+            } else if (c->nt_pack4) {
+                HIPCHK(launch_stage(1, a, true, c->nt_pack4, c->lds_pack4, st));
+            } else {
+                HIPCHK(launch_stage(1, a, true, c->nt_pack, c->lds_pack, st));
+            }
             a.grid_reserve = 0;
         }
         if (n_tail) {
@@ -507,6 +523,22 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
                                                          : packw_layout(c->C, c->B, c->nt_pack4 / (64u * n_out), c->image_bytes, packw_dbuf).total;
         c->crc_hmax4 = ((c->image_bytes / 4u + 2u * c->nt_pack4 - 1u) / (2u * c->nt_pack4)) | 1u;
     }
+    // Frames whose single-buffered k_packw staging admits one workgroup per CU and whose analysis
+    // runs in channel halves are packed in channel halves too (two workgroups per CU, see k_packw)
+    if (c->ana_split && use_packw && !packw_dbuf) {
+        const uint32_t ch = c->C / 2u;
+        const uint32_t img = fg_round16(frame_bound_bytes(kBlock, ch, c->bits, false) + 16u);
+        const uint32_t lh = packw_layout(ch, c->B, 2u, img, false).total;
+        bool on = 2u * lh <= 160u * 1024u;
+        if (const char *e = std::getenv("FLACGPU_PACK_SPLIT")) on = on && e[0] != '0';  // A/B knob
+        if (on) {
+            c->pack_split = true;
+            c->nt_psplit = 64u * ch * 2u;
+            c->lds_psplit = lh;
+            c->image_split = img;
+            c->crc_hmaxs = ((img / 4u + 2u * c->nt_psplit - 1u) / (2u * c->nt_psplit)) | 1u;
+        }
+    }
     if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u ||
         c->lds_pack4 > 160u * 1024u) {
         delete c;
@@ -539,6 +571,16 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     std::vector<uint16_t> pw4((size_t)HM4 * T4 + 1);
     for (uint32_t h = 1; h <= HM4; h++)
         for (uint32_t t = 0; t < T4; t++) pw4[(size_t)(h - 1) * T4 + t] = (uint16_t)crc_zpow(64ull * h * (T4 - 1u - t));
+
+    std::vector<uint16_t> pws((size_t)c->crc_hmaxs * c->nt_psplit + 1), x8(24);
+    for (uint32_t h = 1; h <= c->crc_hmaxs; h++)
+        for (uint32_t t = 0; t < c->nt_psplit; t++)
+            pws[(size_t)(h - 1) * c->nt_psplit + t] = (uint16_t)crc_zpow(64ull * h * (c->nt_psplit - 1u - t));
+    for (uint32_t i = 0; i < 24; i++) x8[i] = (uint16_t)crc_zpow(8ull << i);
+    if (hipMalloc(&c->d_crc_pows, pws.size() * 2) || hipMalloc(&c->d_crc_x8, 48) ||
+        hipMemcpy(c->d_crc_pows, pws.data(), pws.size() * 2, hipMemcpyHostToDevice) ||
+        hipMemcpy(c->d_crc_x8, x8.data(), 48, hipMemcpyHostToDevice))
+        return fail(FLACGPU_ERR_DEVICE);
 
     const uint64_t F = c->max_frames;
     c->pcm_cap = F * (uint64_t)kBlock * c->C * c->B + 64;
@@ -583,6 +625,8 @@ void flacgpu_close(flacgpu_ctx *c) {
     hipFree(c->d_out);
     hipFree(c->d_records);
     hipFree(c->d_stamps);
+    hipFree(c->d_crc_pows);
+    hipFree(c->d_crc_x8);
     hipFree(c->d_md5_state);
     hipFree(c->d_md5_blocks);
     if (c->fork) hipEventDestroy(c->fork);

@@ -95,7 +95,10 @@ struct FrameDesc {
 };
 static_assert(sizeof(FrameDesc) == 32, "FrameDesc layout");
 
-__host__ __device__ constexpr uint32_t desc_stride(uint32_t n_out) { return 32u + n_out * (uint32_t)sizeof(SubDesc); }
+// descriptor of a frame: FrameDesc, n_out SubDesc, then 32 B of channel-half pack hand-off
+// (k_packw split mode: the halves' CRC partials and shared byte, and the arrival ticket)
+__host__ __device__ constexpr uint32_t desc_side_off(uint32_t n_out) { return 32u + n_out * (uint32_t)sizeof(SubDesc); }
+__host__ __device__ constexpr uint32_t desc_stride(uint32_t n_out) { return desc_side_off(n_out) + 32u; }
 
 struct EncodeArgs {
     const uint8_t *pcm;         // device PCM base
@@ -134,6 +137,7 @@ struct EncodeArgs {
                                 // = the half's count), frame totals by k_frame_totals
     uint32_t grid_reserve;      // host side: persistent workgroups left unlaunched (room for the
                                 // stream-MD5 workgroups queued beside this kernel)
+    const uint16_t *crc_x8;     // [i] = z^(8 * 2^i) mod P, i < 24 (channel-half pack: CRC shift)
 };
 
 }  // namespace fg

@@ -273,12 +273,14 @@ __device__ __forceinline__ void lds_or2(uint32_t addr, uint32_t hi, uint32_t lo)
 
 // Frame image (big-endian words, bit 0 of the frame = bit 31 of word 0) -> out[D, D + fbytes),
 // realigned to the byte offset D: 16 bytes per thread and store, edge units byte-masked.
+// lo > 0: the first lo bytes are left unwritten (out[D + lo, D + fbytes) only).
 __device__ __forceinline__ void store_frame16(const uint32_t *img, uint8_t *out, uint64_t D, uint32_t fbytes,
-                                              uint32_t tid, uint32_t NT) {
+                                              uint32_t tid, uint32_t NT, uint32_t lo = 0) {
     const uint64_t E = D + fbytes;
     const uint32_t sa = (uint32_t)(D & 3u);
     const uint64_t qD = D >> 2;
-    for (uint64_t u = (D >> 4) + tid; u < ((E + 15u) >> 4); u += NT) {
+    const uint64_t DL = D + lo;
+    for (uint64_t u = (DL >> 4) + tid; u < ((E + 15u) >> 4); u += NT) {
         const int32_t m0 = (int32_t)(4u * u - qD);  // image word of the unit's first word (>= -3)
         uint32_t v[4];
         uint32_t prev = m0 >= 1 ? img[m0 - 1] : 0u;
@@ -290,7 +292,7 @@ __device__ __forceinline__ void store_frame16(const uint32_t *img, uint8_t *out,
             prev = lo;
         }
         const uint64_t b0 = 16u * u;
-        if (b0 >= D && b0 + 16u <= E) {
+        if (b0 >= DL && b0 + 16u <= E) {
             *(uint4 *)(out + b0) = make_uint4(v[0], v[1], v[2], v[3]);
         } else {
 #pragma unroll
@@ -298,7 +300,7 @@ __device__ __forceinline__ void store_frame16(const uint32_t *img, uint8_t *out,
 #pragma unroll
                 for (uint32_t b = 0; b < 4; b++) {
                     const uint64_t bb = b0 + 4u * c + b;
-                    if (bb >= D && bb < E) out[bb] = (uint8_t)(v[c] >> (8 * b));
+                    if (bb >= DL && bb < E) out[bb] = (uint8_t)(v[c] >> (8 * b));
                 }
         }
     }
@@ -2433,6 +2435,10 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
     }
     // other full frames: WPS waves per written subframe (fg_packw.hpp); the host marks it by
     // the thread count 64 * n_out * WPS (k_pack runs 64 * n_out)
+    if (stage == 1 && full && a.ch_split) {
+        // channel halves (k_packw split mode): 2 waves per written subframe of the half
+        return launch_persistent(k_packw<B, CLS, 0, LPW, 32, true>, a, threads, lds, st);
+    }
     if (stage == 1 && full) {
         const uint32_t n_out = a.stereo ? 2u : a.channels;
         if (threads == 64u * n_out * 4u) {

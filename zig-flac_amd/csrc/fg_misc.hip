@@ -221,6 +221,8 @@ __global__ void k_frame_totals(EncodeArgs a) {
     uint32_t total = 8u * f->hdr_bytes;
     for (uint32_t c = 0; c < f->n_out; c++) total += sd[c].bits;
     f->total_bits = total;
+    // channel-half pack hand-off word (k_packw split mode) starts empty
+    *(unsigned long long *)((uint8_t *)f + desc_side_off(f->n_out)) = 0ull;
     const uint32_t fbytes = ((total + 7u) >> 3) + 2u;
     if (fbytes + 16u > a.image_bytes) atomicOr(a.err, 1u);
     a.frame_bytes[slot] = fbytes;

@@ -44,23 +44,52 @@ __device__ __forceinline__ uint32_t packw_byte(uint32_t i, uint32_t c, uint32_t 
 // LDS-DMA one frame into the k_packw staging: LDS word k = 64 xi + l of a chunk holds source
 // word k - sub(k), or (pad slot) a dummy; `code` packs sub (2 bits) and the pad flag of every
 // slot xi in 3 bits per lane, computed once per kernel.
+// drh != 0 (channel halves): the staged chunk holds the drh dwords [half drh, half drh + drh) of
+// every 2 drh-dword interchannel row (cw = the half row's dwords x 64), as k_analyze's split mode.
 __device__ __forceinline__ void stage_dma_w(const uint8_t *pcm, uint64_t off, uint32_t *stg, uint32_t cw, uint32_t cst,
-                                            uint32_t code, uint32_t wave, uint32_t NW, uint32_t l) {
+                                            uint32_t code, uint32_t wave, uint32_t NW, uint32_t l, uint32_t drh = 0,
+                                            uint32_t half = 0) {
     const uint32_t *src = (const uint32_t *)(pcm + off);
+    const float inv = drh ? 1.0f / (float)drh : 0.0f;  // x / drh exactly for x < 2^10, drh <= 4
     for (uint32_t ch = wave; ch < 64u; ch += NW) {
 #pragma unroll
         for (uint32_t xi = 0; xi < 9u; xi++) {
             const uint32_t cd = (code >> (3u * xi)) & 7u;
-            const uint32_t so = (cd & 4u) ? 0u : 64u * xi + l - cd;
+            uint32_t so = (cd & 4u) ? 0u : 64u * xi + l - cd;
+            uint32_t base = ch * cw;
+            if (drh) {
+                const uint32_t r = (uint32_t)((float)so * inv);
+                so = r * 2u * drh + half * drh + (so - r * drh);
+                base = ch * 2u * cw;
+            }
             if (64u * xi < cst && 64u * xi + l < cst)
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + ch * cw + so),
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + so),
                                                  (__attribute__((address_space(3))) void *)(stg + ch * cst + 64u * xi), 4,
                                                  0, 0);
         }
     }
 }
 
-template <int B, int CLS, int NC, int LPW, int SPL>
+// z^(8 m) mod P for m < 2^24, wave-parallel: lane i < 24 contributes z^(8 * 2^i) when bit i of
+// m is set, the 32-lane product by a butterfly of table-assisted carry-less multiplies
+__device__ __forceinline__ uint32_t crc_zpow8(uint32_t m, const uint16_t *x8, const uint16_t *crct, uint32_t l) {
+    uint32_t f = (l < 24u && ((m >> l) & 1u)) ? (uint32_t)x8[l] : 1u;
+#pragma unroll
+    for (int d = 1; d < 32; d <<= 1) f = crc_mulmod_t(f, (uint32_t)__shfl_xor((int)f, d), crct);
+    return f;
+}
+
+// SPLIT: channel halves (frames of 4+ independent channels whose staging admits one workgroup
+// per CU, c4): a work item is (frame, half), the workgroup stages only its half's channels and
+// packs its half's subframes into its own image -- half 0 the header and subframes
+// [0, n/2), half 1 the rest, its image starting at the byte that holds its first bit.  The
+// frame's CRC-16 is linear in the message: CRC(frame) = CRC(img0) z^(8 (Lb - e0)) ^ CRC(img1)
+// (init 0: leading zero bytes do not change a CRC), so each half folds its own image, stores
+// its bytes except the one byte both halves share, and hands its CRC partial and its part of
+// that byte to the frame's descriptor; the second to arrive (atomic ticket) writes the shared
+// byte and the CRC.  Two 55-KiB halves per CU overlap one half's DMA / store with the other's
+// compute, where one 101-KiB whole frame per CU ran those phases back to back.
+template <int B, int CLS, int NC, int LPW, int SPL, bool SPLIT = false>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8))) k_packw(EncodeArgs a) {
     using ST = typename Cls<CLS>::S;
     constexpr int KH = LPW > 4 ? LPW : 4;  // history samples (most warm-ups of any predictor)
@@ -70,8 +99,11 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
 
     const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l0 = lane_id();
-    const uint32_t sfi = wave / WPS, hq = wave % WPS;  // written subframe, part
-    const uint32_t C = NC ? (uint32_t)NC : a.channels;
+    const uint32_t sfi = wave / WPS, hq = wave % WPS;  // written subframe (of the half), part
+    const uint32_t NH = NW / WPS;                      // written subframes of this workgroup
+    constexpr uint32_t ssh = SPLIT ? 1u : 0u;
+    const uint32_t C = NC ? (uint32_t)NC : a.channels;  // split: the half's channels
+    const uint32_t drh = SPLIT ? C * (uint32_t)B / 4u : 0u;  // split: dwords of a half row
     const uint32_t CB = C * (uint32_t)B;
     const uint32_t cw = 16u * C * B, cst = packw_cst(C, B, WPS);
     const uint32_t sw = (uint32_t)SPL * CB / 4u;  // words of one lane's sub-chunk
@@ -92,37 +124,50 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     if (blockIdx.x == 0 && tid == 0) a.work_ctr[0] = a.work_ctr[1] = 0u;  // the analysis kernel's queues
     if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
     __syncthreads();
+    const uint32_t n_items = a.n_jobs << ssh;
     uint32_t jidx = blockIdx.x, buf = 0;
     uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
     FrameJob job{}, jn{};
-    if (jidx < a.n_jobs) job = a.jobs[jidx];
-    if (nxt < a.n_jobs) jn = a.jobs[nxt];
-    if (dbuf && jidx < a.n_jobs) stage_dma_w(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, dcode, wave, NW, l0);
+    if (jidx < n_items) job = a.jobs[jidx >> ssh];
+    if (nxt < n_items) jn = a.jobs[nxt >> ssh];
+    if (dbuf && jidx < n_items)
+        stage_dma_w(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, dcode, wave, NW, l0, drh, jidx & ssh);
 #ifdef FG_STAMPS
     uint64_t ph_[16] = {};
     uint64_t tprev_ = __builtin_amdgcn_s_memtime();
 #endif
-    while (jidx < a.n_jobs) {
+    while (jidx < n_items) {
         const uint32_t l = opaque(l0);
+        const uint32_t half = jidx & ssh;
         if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
         uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
         // single buffer: the frame's DMA first, so the descriptor's dependent loads below run
         // under it instead of ahead of it (the previous frame's last barrier freed the buffer)
-        if (!dbuf) stage_dma_w(a.pcm, job.pcm_off, stg, cw, cst, dcode, wave, NW, l);
+        if (!dbuf) stage_dma_w(a.pcm, job.pcm_off, stg, cw, cst, dcode, wave, NW, l, drh, half);
         const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
         const FrameDesc *F = (const FrameDesc *)fd;
         const SubDesc *sd0 = (const SubDesc *)(fd + sizeof(FrameDesc));
-        const SubDesc *sd = sd0 + sfi;
+        const uint32_t sidx = half * NH + sfi;  // this wave's subframe in the frame
+        const SubDesc *sd = sd0 + sidx;
         const uint32_t total_bits = F->total_bits;
-        const uint32_t fbytes = ((total_bits + 7u) >> 3) + 2u;
+        const uint32_t Lt = (total_bits + 7u) >> 3;  // the frame's bytes before the CRC
         const uint64_t D = a.offsets[job.slot];
-        const uint32_t Lb = (total_bits + 7u) >> 3;
+        // split: half 0 ends at bit b0 (header + its subframes); half 1's image starts at byte
+        // b0 / 8 and ends with the frame.  Lb = this image's bytes (whole frame: Lt)
+        uint32_t b0 = 0, base = 0, Lb = Lt;
+        if (SPLIT) {
+            b0 = 8u * F->hdr_bytes;
+            for (uint32_t t = 0; t < NH; t++) b0 += sd0[t].bits;
+            base = half ? (b0 >> 3) : 0u;
+            Lb = half ? Lt - base : (b0 + 7u) >> 3;
+        }
+        const uint32_t fbytes = SPLIT ? Lb : Lt + 2u;  // image bytes this workgroup fills
         const uint32_t W4 = Lb >> 2;
         const uint32_t H = max((W4 + 2u * NT - 1u) / (2u * NT), 1u);  // words per thread / 2
         const uint32_t hcq = min(H, a.crc_hmax4) - 1u;
         const uint32_t crc_pw = a.crc_pow4[hcq * NT + tid];
-        const bool skip = fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap;  // uniform
+        const bool skip = fbytes + 16u > a.image_bytes || D + Lt + 2u > a.out_cap;  // uniform
         const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
                        method = sd->method, cand = sd->cand;
         const uint32_t i0 = hq * 64u * SPL + SPL * l0;  // first sample of this lane
@@ -131,7 +176,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         for (int g = 0; g < NG; g++) pq[g] = sd->params[(i0 + 16u * g) >> (12u - o)];
         const uint32_t lb = sd->lane_bits[l0];
         uint32_t sub_start = 8u * F->hdr_bytes;
-        for (uint32_t t = 0; t < sfi; t++) sub_start += sd0[t].bits;
+        for (uint32_t t = 0; t < sidx; t++) sub_start += sd0[t].bits;
+        sub_start -= 8u * base;
 
         // ---- 1. PCM (double-buffered: DMA'd during the previous frame) -> samples
         STAMP(7);
@@ -140,9 +186,11 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         __syncthreads();
         STAMP(0);
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
-        if (dbuf && nxt < a.n_jobs) stage_dma_w(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, dcode, wave, NW, l);
+        if (dbuf && nxt < n_items)
+            stage_dma_w(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, dcode, wave, NW, l, drh,
+                        nxt & ssh);
         FrameJob jnn{};
-        if (nn < a.n_jobs) jnn = a.jobs[nn];
+        if (nn < n_items) jnn = a.jobs[nn >> ssh];
         if (skip) {
             if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
             __syncthreads();
@@ -155,7 +203,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         {
             const uint32_t ia = SPL * l + hq * 64u * SPL;  // == i0, from the opaque lane id
             const uint32_t kind = stereo ? cand : 0u;        // 0 plain channel, 1 R, 2 mid, 3 side
-            const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand;
+            const uint32_t chan = stereo ? (cand == 1 ? 1u : 0u) : cand - half * C;  // split: of the half
             // the lane's own samples sit in one sub-chunk: a per-lane base plus immediates
             const uint32_t lbase = packw_byte<B, SPL>(ia, 0u, cst, sw, CB);
             auto fill = [&](auto KD) {
@@ -197,7 +245,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         for (uint32_t i = tid; i < Wz; i += NT) img[i] = 0;
         STAMP(2);
 
-        // ---- 2. waste shift and residuals, lengths of this lane's codes
+        // ---- 2. waste shift and residuals, lengths of this lane's codes (k_packw)
         const uint32_t bps = bd - w;
         if (type != 0 && w != 0) {
 #pragma unroll
@@ -284,7 +332,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         const uint32_t lane_off = wave_incl_scan32(len) - len;
         bar_lds();  // image zeroed
         STAMP(3);
-        if (tid < 4) {
+        if (tid < 4 && half == 0) {
             const uint32_t hv = F->hdr[tid];
             if (hv) atomicOr(&img[tid], hv);
         }
@@ -392,23 +440,61 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             if (l == 0) misc[wave] = contrib;
         }
         bar_lds();
-        if (tid == 0) {
+        if (!SPLIT) {
+            if (tid == 0) {
+                uint32_t crc = 0;
+                for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
+                for (uint32_t b = W4 * 4u; b < Lb; b++)
+                    crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+                put_bits(img, Lb * 8u, crc, 16);
+            }
+            bar_lds();
+            STAMP(5);
+
+            // ---- 5. image -> out[D, D + fbytes)
+            store_frame16(img, a.out, D, fbytes, tid, NT);
+        } else if (wave == 0) {
+            // ---- 4b. this half's CRC partial (half 0: shifted past the bytes after its image)
             uint32_t crc = 0;
             for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
-            for (uint32_t b = W4 * 4u; b < Lb; b++)
-                crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
-            put_bits(img, Lb * 8u, crc, 16);
+            if (l == 0)
+                for (uint32_t b = W4 * 4u; b < Lb; b++)
+                    crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+            crc = (uint32_t)__shfl((int)crc, 0);
+            if (half == 0) crc = crc_mulmod_t(crc, crc_zpow8(Lt - Lb, a.crc_x8, crct, l), crct);
+            const bool shared = (b0 & 7u) != 0;  // one byte holds bits of both halves
+            const uint32_t sb = shared ? (half ? img[0] >> 24 : (img[(Lb - 1u) >> 2] >> (24 - 8 * ((Lb - 1u) & 3))) & 255u)
+                                       : 0u;
+            // hand-off in ONE 64-bit word per frame, half h in bits [32 h, 32 h + 32): present bit 31,
+            // shared-byte bits 16..23, CRC partial 0..15.  A single device-scope atomicOr publishes a
+            // half and returns the other's: no fence (a release fence writes back the XCD's L2,
+            // which the pack's output stores keep full -- measured 2.2x slower)
+            unsigned long long *side =
+                (unsigned long long *)(a.desc + (uint64_t)job.slot * a.desc_stride + desc_side_off(F->n_out));
+            if (l == 0) {
+                const unsigned long long mine = (unsigned long long)(0x80000000u | (sb << 16) | (crc & 0xFFFFu)) << (32u * half);
+                const unsigned long long old = atomicOr(side, mine);
+                const uint32_t other = (uint32_t)(old >> (32u * (half ^ 1u)));
+                if (other & 0x80000000u) {  // the other half is already in: write the shared byte and the CRC
+                    const uint32_t c16 = (crc ^ other) & 0xFFFFu;
+                    if (shared) a.out[D + (b0 >> 3)] = (uint8_t)(sb | (other >> 16));
+                    a.out[D + Lt] = (uint8_t)(c16 >> 8);
+                    a.out[D + Lt + 1u] = (uint8_t)c16;
+                }
+            }
         }
-        bar_lds();
-        STAMP(5);
-
-        // ---- 5. image -> out[D, D + fbytes)
-        store_frame16(img, a.out, D, fbytes, tid, NT);
+        if (SPLIT) {
+            // ---- 5b. this half's bytes of out[D, D + Lt), the shared byte left to the hand-off
+            const bool shared = (b0 & 7u) != 0;
+            if (half == 0) store_frame16(img, a.out, D, shared ? Lb - 1u : Lb, tid, NT);
+            else store_frame16(img, a.out, D + base, Lb, tid, NT, shared ? 1u : 0u);
+            STAMP(5);
+        }
         // single buffer: the next frame's staging overwrites the image
         if (!dbuf) __syncthreads();
         STAMP(6);
         jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
-    }  // persistent frame loop
+    }  // persistent frame loop (k_packw)
 #ifdef FG_STAMPS
     if (l0 == 0 && a.stamps)
         for (int i = 0; i < 11; i++) atomicAdd(&a.stamps[16 + i], (unsigned long long)ph_[i]);
