@@ -667,13 +667,17 @@ def main():
     total_bytes = int(w.d_tot[0].item())
     pcm_bytes = args.frames * 4096 * fb
     per_launch = {name: (v[1] / v[0]) / 1e3 for name, v in kt.items() if v[0]}
+    # launches per step: 1, or the range count of the overlapped schedule (FLACGPU_OVERLAP, each
+    # range's analysis / scan / pack is its own launch); bytes per launch scale with it
+    lps = {name: max(1, round(v[0] / args.steps)) for name, v in kt.items() if v[0]}
     # The dominant kernel bounds the step: the encode kernels run in sequence on the step's stream
     # (analysis -> scan -> pack), the MD5 beside them on its own stream.  While the MD5's chain is
     # shorter than the encode path it is off the critical path, and the dominant kernel is the
     # longest encode kernel; otherwise the MD5.  Every kernel's own roofline is in `kernels`.
-    path_s = sum(per_launch.get(k, 0.0) for k in ("analyze", "analyze_tail", "scan", "pack"))
+    path_s = sum(per_launch.get(k, 0.0) * lps.get(k, 1) for k in ("analyze", "analyze_tail", "scan", "pack"))
     key = workload_key(args)
     algo = {"analyze": pcm_bytes, "pack": pcm_bytes + int(fbytes.sum()), "md5": pcm_bytes}
+    algo = {k: v // lps.get(k, 1) for k, v in algo.items()}
 
     def kernel_roofline(k):
         avg = per_launch[k]
@@ -690,7 +694,7 @@ def main():
 
     enc_k = [k for k in ("analyze", "pack") if k in per_launch]
     md5_off_path = "md5" not in per_launch or per_launch["md5"] < path_s
-    dom = max(enc_k, key=lambda k: per_launch[k]) if md5_off_path else "md5"
+    dom = max(enc_k, key=lambda k: per_launch[k] * lps[k]) if md5_off_path else "md5"
     rk = {k: kernel_roofline(k) for k in ("analyze", "pack", "md5") if k in per_launch}
     algo_bytes, avg_s = algo[dom], per_launch[dom]
     achieved = algo_bytes / avg_s / 1e9
@@ -767,6 +771,7 @@ def main():
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "launches": kt[dom][0],
+                "launches_per_step": lps[dom],
                 "encode_path_gbs": round((pcm_bytes + int(fbytes.sum())) / path_s / 1e9, 2) if path_s > 0 else None,
                 "issue": issue,
                 "selection": "longest encode kernel on the step's critical path (the MD5 chain, "
@@ -774,7 +779,7 @@ def main():
                              if md5_off_path else "the MD5 chain is longer than the encode path: it bounds the step",
                 "kernels": rk,
             },
-            "kernel_ms_per_step": {k: round(v[1] / max(v[0], 1), 4) for k, v in kt.items() if v[0]},
+            "kernel_ms_per_step": {k: round(v[1] / args.steps, 4) for k, v in kt.items() if v[0]},
             "output_ok": ok,
             "verified": vinfo,
             "stream_curve": curve,

@@ -331,6 +331,15 @@ typedef struct {
 } flacgpu_frame_record;
 
 int flacgpu_set_records(flacgpu_ctx *ctx, int enable);
+
+/* Encode schedule (no reference counterpart: how the device runs the writeFrame loop).
+ * ranges > 1: each call's full frames are encoded in that many frame ranges, the analysis of
+ * range i+1 beside the scan + pack of range i on a second HIP stream, the two persistent grids
+ * capped at ana_per_cu / pack_per_cu workgroups per CU (0 = no cap); calls with fewer than
+ * ranges * min_frames full frames use fewer ranges.  ranges <= 1: one analysis, scan and pack
+ * launch per call.  Output bytes are the same either way. */
+int flacgpu_set_overlap(flacgpu_ctx *ctx, uint32_t ranges, uint32_t ana_per_cu, uint32_t pack_per_cu,
+                        uint32_t min_frames);
 int flacgpu_get_records(flacgpu_ctx *ctx, flacgpu_frame_record *out, uint64_t max_frames, uint64_t *n_frames);
 
 #ifdef __cplusplus

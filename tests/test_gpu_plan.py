@@ -317,3 +317,50 @@ def test_md5_kernels_ragged(kernel, monkeypatch):
     for s, (_, _, dig) in enumerate(res):
         want = hashlib.md5(bytes(buf[offs[s]:offs[s] + 4 * lengths[s]])).digest()
         assert dig == want, f"stream {s} ({lengths[s]} samples): MD5 kernel {kernel}"
+
+
+# ---- the overlapped encode schedule (flacgpu_set_overlap): the full frames in ranges, the
+# analysis of range i+1 beside the scan (carried base) + pack of range i on a second HIP stream,
+# per-range ticket sets, tail frames analysed first and packed last.  Same bytes as the oracle.
+@pytest.mark.parametrize("ch,bits,rate,lpc", [(2, 16, 44100, 0), (8, 24, 96000, 0), (2, 24, 96000, 8),
+                                              (2, 32, 192000, 0), (1, 16, 48000, 0)])
+@pytest.mark.parametrize("ranges,ana,pack", [(4, 2, 2), (3, 0, 0), (7, 1, 3)])
+def test_overlapped_schedule_matches_oracle(ch, bits, rate, lpc, ranges, ana, pack):
+    fb = ch * (bits // 8)
+    offs, size = _layout(LENGTHS, fb, (4, 8, 12, 0))
+    buf = bytearray(size)
+    pcms = []
+    for s, n in enumerate(LENGTHS):
+        pcm = synth.synth_pcm(n, ch, bits, rate, stream=300 + s) if n else b""
+        buf[offs[s]:offs[s] + len(pcm)] = pcm
+        pcms.append(pcm)
+    with _encoder(ch, bits, rate, lpc_order=lpc) as enc:
+        enc.set_overlap(ranges, ana, pack, min_frames=2)
+        for md5 in ("join", "state"):  # twice: the per-range ticket sets are reused by the second call
+            res, _ = _run_plan(enc, bytes(buf), offs, LENGTHS, md5=md5)
+            for s, (got, sizes, dig) in enumerate(res):
+                ref, ref_sizes, ref_md5 = oracle_ref.encode_stream(pcms[s], ch, bits, rate, lpc=lpc)
+                assert sizes == ref_sizes, f"stream {s}: frame sizes differ"
+                assert got == ref, f"stream {s}: bytes differ"
+                if md5 == "join":
+                    assert dig == ref_md5, f"stream {s}: MD5"
+
+
+def test_overlapped_schedule_many_ranges_and_serial_again():
+    """64 ranges of a long plan, then the serial schedule on the same context (ticket sets shared)."""
+    ch, bits, rate = 2, 16, 44100
+    lengths = [4096 * 16 + 5] * 24 + [4096 * 7] * 8
+    offs, size = _layout(lengths, 4, (0, 8))
+    buf = bytearray(size)
+    pcms = []
+    for s, n in enumerate(lengths):
+        pcm = synth.synth_pcm(n, ch, bits, rate, stream=400 + s)
+        buf[offs[s]:offs[s] + len(pcm)] = pcm
+        pcms.append(pcm)
+    refs = [oracle_ref.encode_stream(p, ch, bits, rate)[:2] for p in pcms]
+    with _encoder(ch, bits, rate, max_frames=512) as enc:
+        for ranges in (64, 0, 5, 1):
+            enc.set_overlap(ranges, 2, 2, min_frames=1)
+            res, _ = _run_plan(enc, bytes(buf), offs, lengths, md5="none")
+            for s, (got, sizes, _) in enumerate(res):
+                assert (got, sizes) == (refs[s][0], refs[s][1]), f"ranges {ranges} stream {s}"

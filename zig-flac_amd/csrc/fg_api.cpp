@@ -25,7 +25,7 @@ hipError_t launch_make_jobs(FrameJob *jobs, uint64_t n_samples, uint32_t block, 
                             uint32_t n_frames, hipStream_t st);
 hipError_t launch_frame_totals(const EncodeArgs &a, hipStream_t st);
 hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, uint64_t *part,
-                       hipStream_t st);
+                       hipStream_t st, const uint64_t *base = nullptr);
 hipError_t launch_md5_streams(const uint8_t *base, const uint64_t *offs, const uint64_t *lens, const uint8_t *fin,
                               uint32_t n, Md5State *states, uint8_t *digests, hipStream_t st, int kernel, int prio);
 hipError_t launch_advance_jobs(FrameJob *jobs, uint64_t n, uint64_t delta, hipStream_t st);
@@ -119,6 +119,13 @@ struct flacgpu_ctx {
     int md5_reserve = -1;  // 1: the analysis grid leaves one workgroup slot per stream-MD5 workgroup
                            //    queued beside it, 2: the pack grid too, 0: none, -1: auto (A/B knob)
     uint32_t grid_reserve = 0;  // per call: slots the next analysis / pack launches leave free
+    // overlapped encode (encode_core): the full frames in `ovl_chunks` ranges, the analysis of
+    // range i+1 on `stream` beside the scan + pack of range i on `ovl`, each grid capped to
+    // ovl_ana / ovl_pack workgroups per CU so both are resident on every CU
+    uint32_t ovl_chunks = 0, ovl_ana = 2, ovl_pack = 2, ovl_min_frames = 4096;
+    bool xcd_queue = true;  // split analysis: per-XCD item queues (fg_device.hpp xcd_ticket)
+    hipStream_t ovl = nullptr;
+    uint64_t *d_cum = nullptr;  // [chunk] bytes of the frames before the chunk's slot range
     HostMd5 host_md5;
     uint32_t *d_md5_state = nullptr;
     uint32_t *d_md5_blocks = nullptr;
@@ -129,6 +136,8 @@ struct flacgpu_ctx {
 
 // device MD5 engine: whole blocks move through one bounded device buffer
 constexpr uint64_t kMd5ChunkBlocks = (64ull << 20) / 64;
+// overlapped encode: at most this many frame ranges per call (one ticket set of 4 u32 each)
+constexpr uint32_t kOvlMaxChunks = 64;
 
 struct flacgpu_plan {
     flacgpu_ctx *ctx = nullptr;
@@ -141,6 +150,7 @@ struct flacgpu_plan {
     uint64_t md5_max_len = 0;      // longest stream segment (bytes): the MD5 chain of one call
     uint64_t max_number = 0;       // largest frame number in the table (u36 check on advance)
     std::vector<uint64_t> first_frame;
+    std::vector<uint32_t> full_slots;  // slot of each full job (host copy: ranges of the overlapped encode)
     uint64_t out_bound = 0;
     uint8_t *d_desc = nullptr;  // per-plan descriptor area when larger than the context's
 };
@@ -227,10 +237,18 @@ uint64_t frames_for(uint64_t n_samples, uint32_t bs) { return (n_samples + bs - 
 
 // Queue the encode of n_full full frames (jobs[0..n_full)) and n_tail short ones
 // (jobs[n_full..)): analysis (descriptors + exact sizes), scan (byte offsets),
-// pack (frames written at their offsets in d_out).
+// pack (frames written at their offsets in d_out).  full_slots: the slot of each full job
+// (NULL: slot == job index); full jobs are in increasing slot order.
+//
+// Overlapped schedule (c->ovl_chunks > 1 and enough full frames): the tail frames are analysed
+// first, then the full frames in K ranges: the analysis of range i+1 runs on `st` while the scan
+// of range i's slot span (carried base: the bytes before it) and its pack run on c->ovl, each
+// persistent grid capped per CU so that an analysis grid and a pack grid share every CU (the
+// analysis is VALU/issue bound, the pack LDS/latency bound).  Each range has its own set of
+// frame-queue tickets.  Output bytes are identical to the serial schedule.
 int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, uint64_t n_full, uint64_t n_tail,
                 uint8_t *d_desc, uint32_t *d_fbytes, uint8_t *d_out, uint64_t out_cap, uint64_t *d_offsets,
-                uint64_t *d_total, hipStream_t st) {
+                uint64_t *d_total, hipStream_t st, const uint32_t *full_slots = nullptr) {
     const uint64_t n_frames = n_full + n_tail;
     if (n_frames == 0) {
         HIPCHK(hipMemsetAsync(d_total, 0, sizeof(uint64_t), st));
@@ -268,69 +286,128 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.records = c->records_on ? c->d_records : nullptr;
     a.stamps = c->d_stamps;
     a.crc_x8 = c->d_crc_x8;
-    if (n_full) {
-        Timed t(c, FLACGPU_K_ANALYZE, st);
-        a.jobs = d_jobs;
-        a.n_jobs = (uint32_t)n_full;
-        a.grid_reserve = c->grid_reserve;
+
+    // full-frame analysis of jobs[j0, j0 + n) with ticket set `set`
+    auto analyze_full = [&](uint64_t j0, uint64_t n, uint32_t set, uint32_t per_cu, hipStream_t s) -> int {
+        Timed t(c, FLACGPU_K_ANALYZE, s);
+        EncodeArgs h = a;
+        h.jobs = d_jobs + j0;
+        h.n_jobs = (uint32_t)n;
+        h.work_ctr = c->d_ctr + kCtrSet * set;
+        h.grid_reserve = c->grid_reserve;
+        h.grid_per_cu = per_cu;
         if (c->ana_split) {
-            a.channels = c->C / 2u;
-            a.ch_split = 1;
-            HIPCHK(launch_stage(0, a, true, c->nt_split, c->lds_split, st));
-            HIPCHK(launch_frame_totals(a, st));
-            a.channels = c->C;
-            a.ch_split = 0;
+            h.channels = c->C / 2u;
+            h.ch_split = 1;
+            h.xcd_queue = c->xcd_queue ? 1u : 0u;
+            HIPCHK(launch_stage(0, h, true, c->nt_split, c->lds_split, s));
+            HIPCHK(launch_frame_totals(h, s));
         } else {
-            HIPCHK(launch_stage(0, a, true, c->nt, c->lds, st));
+            HIPCHK(launch_stage(0, h, true, c->nt, c->lds, s));
         }
-        a.grid_reserve = 0;
+        return FLACGPU_OK;
+    };
+    auto pack_full = [&](uint64_t j0, uint64_t n, uint32_t set, uint32_t per_cu, hipStream_t s) -> int {
+        Timed t(c, FLACGPU_K_PACK, s);
+        EncodeArgs h = a;
+        h.jobs = d_jobs + j0;
+        h.n_jobs = (uint32_t)n;
+        h.work_ctr = c->d_ctr + kCtrSet * set;
+        h.grid_reserve = c->md5_reserve == 2 ? c->grid_reserve : 0u;
+        h.grid_per_cu = per_cu;
+        if (c->pack_split) {
+            h.channels = c->C / 2u;
+            h.ch_split = 1;
+            h.image_bytes = c->image_split;
+            h.crc_pow4 = c->d_crc_pows;
+            h.crc_hmax4 = c->crc_hmaxs;
+            HIPCHK(launch_stage(1, h, true, c->nt_psplit, c->lds_psplit, s));
+        } else if (c->nt_pack4) {
+            HIPCHK(launch_stage(1, h, true, c->nt_pack4, c->lds_pack4, s));
+        } else {
+            HIPCHK(launch_stage(1, h, true, c->nt_pack, c->lds_pack, s));
+        }
+        return FLACGPU_OK;
+    };
+    auto analyze_tail = [&](hipStream_t s) -> int {
+        Timed t(c, FLACGPU_K_ANALYZE_TAIL, s);
+        EncodeArgs h = a;
+        h.jobs = d_jobs + n_full;
+        h.n_jobs = (uint32_t)n_tail;
+        HIPCHK(launch_stage(0, h, false, c->nt, c->lds_tail, s));
+        return FLACGPU_OK;
+    };
+    auto pack_tail = [&](hipStream_t s) -> int {
+        Timed t(c, FLACGPU_K_PACK, s);
+        EncodeArgs h = a;
+        h.jobs = d_jobs + n_full;
+        h.n_jobs = (uint32_t)n_tail;
+        HIPCHK(launch_stage(1, h, false, c->nt_pack, c->lds_pack, s));
+        return FLACGPU_OK;
+    };
+    // the multi-workgroup scan's per-block sums: a grow-only context buffer
+    const uint32_t nb = (uint32_t)((n_frames + 4095u) / 4096u);
+    if (nb > c->scan_part_cap) {
+        hipFree(c->d_scan_part);
+        c->d_scan_part = nullptr;
+        c->scan_part_cap = 0;
+        HIPCHK(hipMalloc(&c->d_scan_part, (size_t)nb * 8u));
+        c->scan_part_cap = nb;
     }
-    if (n_tail) {
-        Timed t(c, FLACGPU_K_ANALYZE_TAIL, st);
-        a.jobs = d_jobs + n_full;
-        a.n_jobs = (uint32_t)n_tail;
-        HIPCHK(launch_stage(0, a, false, c->nt, c->lds_tail, st));
+
+    uint32_t K = c->ovl_chunks;
+    if (K > kOvlMaxChunks) K = kOvlMaxChunks;
+    while (K > 1 && n_full / K < c->ovl_min_frames) K--;
+    if (K > 1) {
+        int rc;
+        if (n_tail && (rc = analyze_tail(st))) return rc;
+        auto slot_of = [&](uint64_t j) -> uint64_t { return full_slots ? full_slots[j] : j; };
+        auto j_begin = [&](uint32_t i) -> uint64_t { return n_full * i / K; };
+        std::vector<hipEvent_t> evs;
+        auto release = [&]() {
+            for (auto e : evs) c->event_pool.push_back(e);
+        };
+        for (uint32_t i = 0; i < K; i++) {
+            const uint64_t j0 = j_begin(i), j1 = j_begin(i + 1);
+            if ((rc = analyze_full(j0, j1 - j0, i, c->ovl_ana, st))) return release(), rc;
+            hipEvent_t ev = get_event(c);
+            if (!ev) return release(), FLACGPU_ERR_DEVICE;
+            evs.push_back(ev);
+            if (hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(c->ovl, ev, 0) != hipSuccess)
+                return release(), FLACGPU_ERR_DEVICE;
+            // the slot span of range i: from its first full job (0 for the first range) to the next
+            // range's first full job (n_frames for the last); tail slots inside it were analysed first
+            const uint64_t s0 = i == 0 ? 0 : slot_of(j0), s1 = i + 1 == K ? n_frames : slot_of(j1);
+            {
+                Timed t(c, FLACGPU_K_SCAN, c->ovl);
+                if (i == 0 && hipMemsetAsync(c->d_cum, 0, sizeof(uint64_t), c->ovl) != hipSuccess)
+                    return release(), FLACGPU_ERR_DEVICE;
+                const hipError_t e = launch_scan(d_fbytes + s0, d_offsets + s0, i + 1 == K ? d_total : c->d_cum + i + 1,
+                                                 (uint32_t)(s1 - s0), c->d_scan_part, c->ovl, c->d_cum + i);
+                if (e != hipSuccess) return release(), hip_err(e);
+            }
+            if ((rc = pack_full(j0, j1 - j0, i, c->ovl_pack, c->ovl))) return release(), rc;
+        }
+        if (n_tail && (rc = pack_tail(c->ovl))) return release(), rc;
+        // st continues after the last pack
+        hipEvent_t done = get_event(c);
+        if (!done) return release(), FLACGPU_ERR_DEVICE;
+        evs.push_back(done);
+        if (hipEventRecord(done, c->ovl) != hipSuccess || hipStreamWaitEvent(st, done, 0) != hipSuccess)
+            return release(), FLACGPU_ERR_DEVICE;
+        release();  // the waits are enqueued: the events can be recorded again
+        return FLACGPU_OK;
     }
+
+    int rc;
+    if (n_full && (rc = analyze_full(0, n_full, 0, 0, st))) return rc;
+    if (n_tail && (rc = analyze_tail(st))) return rc;
     {
         Timed t(c, FLACGPU_K_SCAN, st);
-        // multi-workgroup scan: per-block sums in a grow-only context buffer
-        const uint32_t nb = (uint32_t)((n_frames + 4095u) / 4096u);
-        if (nb > c->scan_part_cap) {
-            hipFree(c->d_scan_part);
-            c->d_scan_part = nullptr;
-            c->scan_part_cap = 0;
-            HIPCHK(hipMalloc(&c->d_scan_part, (size_t)nb * 8u));
-            c->scan_part_cap = nb;
-        }
         HIPCHK(launch_scan(d_fbytes, d_offsets, d_total, (uint32_t)n_frames, c->d_scan_part, st));
     }
-    {
-        Timed t(c, FLACGPU_K_PACK, st);
-        if (n_full) {
-            a.jobs = d_jobs;
-            a.n_jobs = (uint32_t)n_full;
-            a.grid_reserve = c->md5_reserve == 2 ? c->grid_reserve : 0u;
-            if (c->pack_split) {
-                EncodeArgs h = a;
-                h.channels = c->C / 2u;
-                h.ch_split = 1;
-                h.image_bytes = c->image_split;
-                h.crc_pow4 = c->d_crc_pows;
-                h.crc_hmax4 = c->crc_hmaxs;
-                HIPCHK(launch_stage(1, h, true, c->nt_psplit, c->lds_psplit, st));
-            } else if (c->nt_pack4) {
-                HIPCHK(launch_stage(1, a, true, c->nt_pack4, c->lds_pack4, st));
-            } else {
-                HIPCHK(launch_stage(1, a, true, c->nt_pack, c->lds_pack, st));
-            }
-            a.grid_reserve = 0;
-        }
-        if (n_tail) {
-            a.jobs = d_jobs + n_full;
-            a.n_jobs = (uint32_t)n_tail;
-            HIPCHK(launch_stage(1, a, false, c->nt_pack, c->lds_pack, st));
-        }
-    }
+    if (n_full && (rc = pack_full(0, n_full, 0, 0, st))) return rc;
+    if (n_tail && (rc = pack_tail(st))) return rc;
     return FLACGPU_OK;
 }
 
@@ -494,6 +571,12 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);      // A/B knob
     if (const char *e = std::getenv("FLACGPU_MD5_RESERVE")) c->md5_reserve = std::atoi(e);  // A/B knob
     if (const char *e = std::getenv("FLACGPU_MD5_DIAG")) c->md5_prio |= std::atoi(e) << 8;  // diagnostics
+    // overlapped encode: ranges per call, workgroups per CU of the analysis / pack grids (A/B knobs)
+    if (const char *e = std::getenv("FLACGPU_OVERLAP")) c->ovl_chunks = (uint32_t)std::atoi(e);
+    if (const char *e = std::getenv("FLACGPU_XCD_QUEUE")) c->xcd_queue = e[0] != '0';  // A/B knob
+    if (const char *e = std::getenv("FLACGPU_OVL_ANA")) c->ovl_ana = (uint32_t)std::atoi(e);
+    if (const char *e = std::getenv("FLACGPU_OVL_PACK")) c->ovl_pack = (uint32_t)std::atoi(e);
+    if (const char *e = std::getenv("FLACGPU_OVL_MIN")) c->ovl_min_frames = (uint32_t)std::max(1, std::atoi(e));
     c->lds_pack = pack_layout(c->C, c->B, c->image_bytes, c->pack_dbuf).total;
     // CRC fold: half-segments of H words (odd), H <= ceil(image words / (2 * pack threads))
     c->crc_hmax = ((c->image_bytes / 4u + 2u * c->nt_pack - 1u) / (2u * c->nt_pack)) | 1u;
@@ -552,6 +635,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&c->dl, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    if (hipStreamCreateWithFlags(&c->ovl, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
 
@@ -587,7 +671,8 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     c->out_cap = F * (uint64_t)c->image_bytes;
     if (hipMalloc(&c->d_crc_tab, 2048 * 2) || hipMalloc(&c->d_crc_pow, pw.size() * 2) ||
         hipMalloc(&c->d_crc_pow4, pw4.size() * 2) ||
-        hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) || hipMalloc(&c->d_ctr, 16) ||
+        hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) || hipMalloc(&c->d_ctr, 4u * kCtrSet * kOvlMaxChunks) ||
+        hipMalloc(&c->d_cum, 8u * (kOvlMaxChunks + 1u)) ||
         hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_desc, F * (uint64_t)c->desc_stride) ||
         hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
         hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16) || hipMalloc(&c->d_stamps, 32 * 8))
@@ -595,7 +680,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (hipMemcpy(c->d_crc_tab, tab.data(), 4096, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_pow, pw.data(), pw.size() * 2, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_pow4, pw4.data(), pw4.size() * 2, hipMemcpyHostToDevice) ||
-        hipMemcpy(c->d_crc_join, pj.data(), pj.size() * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) || hipMemset(c->d_ctr, 0, 16) ||
+        hipMemcpy(c->d_crc_join, pj.data(), pj.size() * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) || hipMemset(c->d_ctr, 0, 4u * kCtrSet * kOvlMaxChunks) ||
         hipMemset(c->d_stamps, 0, 32 * 8))
         return fail(FLACGPU_ERR_DEVICE);
     flacgpu_md5_init(c);
@@ -616,6 +701,7 @@ void flacgpu_close(flacgpu_ctx *c) {
     hipFree(c->d_scan_part);
     hipFree(c->d_err);
     hipFree(c->d_ctr);
+    hipFree(c->d_cum);
     hipFree(c->d_jobs);
     hipFree(c->d_desc);
     hipFree(c->d_fbytes);
@@ -633,6 +719,7 @@ void flacgpu_close(flacgpu_ctx *c) {
     if (c->join) hipEventDestroy(c->join);
     if (c->aux) hipStreamDestroy(c->aux);
     if (c->dl) hipStreamDestroy(c->dl);
+    if (c->ovl) hipStreamDestroy(c->ovl);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -948,6 +1035,7 @@ int flacgpu_plan_create_segments(flacgpu_ctx *c, uint32_t n_streams, const uint6
                 j.n = (uint32_t)std::min<uint64_t>(bs, samples[s] - f * bs);
                 j.slot = (uint32_t)slot;
                 (j.n == (uint32_t)kBlock ? full : tail).push_back(j);
+                if (j.n == (uint32_t)kBlock) p->full_slots.push_back(j.slot);
             }
         }
         full.insert(full.end(), tail.begin(), tail.end());
@@ -1056,7 +1144,7 @@ int flacgpu_encode_plan_device_ex(flacgpu_ctx *c, const flacgpu_plan *p, const v
     const bool reserve = c->md5_reserve > 0 || (c->md5_reserve < 0 && p->md5_max_len >= (256u << 10));
     c->grid_reserve = (md5 && reserve) ? md5_workgroups(p->n_streams, c->md5_kernel) : 0u;
     int rc = encode_core(c, (const uint8_t *)d_pcm, p->d_jobs, p->n_full, p->n_tail, desc, d_frame_bytes, d_out,
-                         out_cap, d_frame_offsets, d_total, st);
+                         out_cap, d_frame_offsets, d_total, st, p->full_slots.data());
     c->grid_reserve = 0;
     if (rc) return rc;
     if (join && md5) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
@@ -1116,6 +1204,16 @@ int flacgpu_reset_timing(flacgpu_ctx *c) {
         c->launches[k] = 0;
         c->ms[k] = 0;
     }
+    return FLACGPU_OK;
+}
+
+int flacgpu_set_overlap(flacgpu_ctx *c, uint32_t ranges, uint32_t ana_per_cu, uint32_t pack_per_cu,
+                        uint32_t min_frames) {
+    if (!c || ranges > kOvlMaxChunks || min_frames == 0) return FLACGPU_ERR_INVALID_INPUT;
+    c->ovl_chunks = ranges;
+    c->ovl_ana = ana_per_cu;
+    c->ovl_pack = pack_per_cu;
+    c->ovl_min_frames = min_frames;
     return FLACGPU_OK;
 }
 

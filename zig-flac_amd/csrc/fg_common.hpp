@@ -11,6 +11,7 @@ constexpr int kLaneSamples = 64;   // samples per lane: one wave == one 4096-sam
 constexpr int kMaxPartOrder = 8;   // rice.MAX_ORDER (rice.zig:13)
 constexpr int kParamBytes = 512;   // params of all orders 0..8: offset (1<<o)-1 (511 used)
 constexpr int kCrcThreadsMax = 512;
+constexpr uint32_t kCtrSet = 16;    // u32 tickets per work_ctr set (reset_analysis_tickets)
 constexpr uint32_t kMd5StreamsPerWg = 256;  // k_md5_streams workgroup size (one stream per lane)
 // LPC (build-defined extension; the reference has none, readme.md:27): orders
 // 1..12 on the GPU path (the FLAC subset limit), 15-bit coefficients.
@@ -122,8 +123,8 @@ struct EncodeArgs {
     const uint64_t *offsets;    // [slot] byte offset of the frame in out (scan)
     uint8_t *out;               // contiguous output bitstream
     uint64_t out_cap;
-    uint32_t *work_ctr;         // 4 frame-queue tickets: analysis full/tail, pack full/tail (each
-                                // kernel zeroes the other stage's pair for its next launch)
+    uint32_t *work_ctr;         // kCtrSet frame-queue tickets: analysis full/tail, pack full/tail,
+                                // per-XCD split-analysis queues (each stage zeroes the other's)
     uint32_t *err;              // device error word (0 = ok; bit 0 invariant, bit 1 output too small)
     const uint16_t *crc_tab;    // 8 x 256: z^40, z^32, z^24, z^16, z^72, z^64, z^56, z^48 byte tables (CRC-16/UMTS)
     const uint16_t *crc_pow;    // [(H-1)*pack_threads + t] = z^(64*H*(T-1-t)) mod P, H = 1..crc_hmax
@@ -138,6 +139,10 @@ struct EncodeArgs {
     uint32_t grid_reserve;      // host side: persistent workgroups left unlaunched (room for the
                                 // stream-MD5 workgroups queued beside this kernel)
     const uint16_t *crc_x8;     // [i] = z^(8 * 2^i) mod P, i < 24 (channel-half pack: CRC shift)
+    uint32_t xcd_queue;         // split analysis: items from per-XCD queues (xcd_ticket, fg_device.hpp)
+    uint32_t grid_per_cu;       // host side: at most this many persistent workgroups per CU (0 = as
+                                // many as fit) -- the overlapped encode shares each CU between an
+                                // analysis grid and a pack grid running on two streams
 };
 
 }  // namespace fg

@@ -531,6 +531,36 @@ __device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint
 }
 
 
+// Frame-queue tickets (EncodeArgs::work_ctr, one set of kCtrSet u32 per overlapped range):
+// [0] analysis full, [1] analysis tail, [2] pack full, [3] pack tail, [8..15] the split
+// analysis's per-XCD queues.  Each stage zeroes the other stage's tickets at its start (the
+// launches of one set are ordered), so no memset precedes a launch.
+__device__ __forceinline__ void reset_analysis_tickets(uint32_t *ctr, uint32_t tid) {
+    if (blockIdx.x == 0 && tid < 16u && (tid < 2u || tid >= 8u)) ctr[tid] = 0u;
+}
+
+// XCD-aware queue of channel-half work items (split analysis, item = 2 frame + half): XCD x
+// owns frames [x n / 8, (x + 1) n / 8) and hands out their items in order from its own counter,
+// so the two halves of a frame -- which fetch the same cache lines of its interleaved rows --
+// go to workgroups of one XCD at about the same time and the second fetch hits that XCD's L2.
+// An exhausted queue passes on to the next XCD's.  Placement is read from the hardware
+// (HW_REG_XCC_ID) and is used for speed only: every item is handed out exactly once whatever
+// the placement.  Returns 0xFFFFFFFF when every queue is empty.
+__device__ __forceinline__ uint32_t xcd_ticket(uint32_t *q, uint32_t n_frames) {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    x &= 7u;
+    for (uint32_t i = 0; i < 8u; i++) {
+        const uint32_t y = (x + i) & 7u;
+        const uint32_t f0 = (uint32_t)(((uint64_t)n_frames * y) >> 3);
+        const uint32_t f1 = (uint32_t)(((uint64_t)n_frames * (y + 1u)) >> 3);
+        if (f1 == f0) continue;
+        const uint32_t t = atomicAdd(&q[y], 1u);
+        if (t < 2u * (f1 - f0)) return 2u * f0 + t;
+    }
+    return 0xFFFFFFFFu;
+}
+
 // Stage one frame's interleaved PCM synchronously (tail frames zero-filled).
 template <bool FULL>
 __device__ __forceinline__ void stage_sync(const uint8_t *pcm, uint64_t off, uint32_t n, uint32_t CB, uint32_t *stg,
@@ -1129,17 +1159,27 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     // while frame i is analysed, so issuing frame i+1's DMA never waits on a global load.
     uint32_t *ctr = a.work_ctr + (FULL ? 0u : 1u);
     if (blockIdx.x == 0 && tid == 0) a.work_ctr[2] = a.work_ctr[3] = 0u;  // the pack kernel's queues
-    if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
-    __syncthreads();
     // Channel halves (a.ch_split, full frames of 4+ independent channels staged single-buffered):
     // a work item is (frame, half); the half's C channels are dwords [half drh, half drh + drh)
     // of every 2 drh-dword interchannel row, so two or three workgroups share a CU where one
     // whole 96-KiB frame would fill its LDS.  The frame-level fields are completed by
-    // k_frame_totals after the launch.
+    // k_frame_totals after the launch.  The items come from the per-XCD queues (xcd_ticket).
     const uint32_t ssh = (FULL && a.ch_split) ? 1u : 0u;
+    const bool xq = ssh && a.xcd_queue;
+    uint32_t *xqc = a.work_ctr + 8;
     const uint32_t drh = ssh ? C * (uint32_t)B / 4u : 0u;
     const uint32_t n_items = a.n_jobs << ssh;
-    uint32_t jidx = blockIdx.x, buf = 0;
+    if (tid == 0) {
+        if (xq) {
+            misc[22] = xcd_ticket(xqc, a.n_jobs);
+            misc[21] = xcd_ticket(xqc, a.n_jobs);
+        } else {
+            misc[22] = blockIdx.x;
+            misc[21] = gridDim.x + atomicAdd(ctr, 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t jidx = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[22]), buf = 0;
     uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
     FrameJob job{}, jn{};
     if (jidx < n_items) job = a.jobs[jidx >> ssh];
@@ -1172,7 +1212,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // staged PCM, and its value is first used at the estimate barrier (step 9): taken at the
         // top of the loop, the vmcnt(0) for the DMA also waited for the atomic's round trip.
         uint32_t tk = 0;
-        if (tid == 0) tk = atomicAdd(ctr, 1u);
+        if (tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
         STAMP(0);
 
         // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
@@ -1774,7 +1814,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             uint32_t *rc = recs + cand * 16u;
             rc[6] = (uint32_t)R.est; rc[7] = (uint32_t)(R.est >> 32);
         }
-        if (tid == 0) misc[20] = gridDim.x + tk;
+        if (tid == 0) misc[20] = tk;
         __syncthreads();
         // the job record of the frame after next (DMA'd at the top of the next frame)
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
@@ -2049,7 +2089,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
     // PCM of frame i+1 arrives in the idle buffer by LDS-DMA and the job record of frame i+2 is
     // loaded, so neither the staging nor the DMA issue waits on a global round trip.
     uint32_t *ctr = a.work_ctr + (FULL ? 2u : 3u);
-    if (blockIdx.x == 0 && tid == 0) a.work_ctr[0] = a.work_ctr[1] = 0u;  // the analysis kernel's queues
+    reset_analysis_tickets(a.work_ctr, tid);  // the analysis kernel's queues
     if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
     __syncthreads();
     uint32_t jidx = blockIdx.x, buf = 0;
@@ -2405,7 +2445,8 @@ static hipError_t launch_persistent(KernelT k, const EncodeArgs &a, uint32_t thr
         if (n_cache < 64) cache[n_cache++] = {(const void *)k, threads, lds, dev, resident, cus};
     }
     uint64_t grid = (uint64_t)a.n_jobs << (a.ch_split ? 1 : 0);  // work items (channel halves: two per frame)
-    uint64_t cap = (uint64_t)resident * (uint64_t)(cus > 0 ? cus : 256);
+    const int per_cu = (a.grid_per_cu && (int)a.grid_per_cu < resident) ? (int)a.grid_per_cu : resident;
+    uint64_t cap = (uint64_t)per_cu * (uint64_t)(cus > 0 ? cus : 256);
     // leave room for workgroups of a kernel running beside this one (the stream MD5): without it
     // the persistent grid takes every slot and the other kernel waits for this one to finish
     if (a.grid_reserve && cap > 4u * (uint64_t)a.grid_reserve) cap -= a.grid_reserve;

@@ -175,11 +175,11 @@ __global__ void __launch_bounds__(1024) k_scan_part(const uint32_t *sizes, uint6
 }
 
 __global__ void __launch_bounds__(1024) k_scan_blocks(const uint32_t *sizes, uint64_t *offsets, uint64_t *total,
-                                                      const uint64_t *part, uint32_t n) {
+                                                      const uint64_t *part, uint32_t n, const uint64_t *base) {
     __shared__ uint64_t wsum[16], bsum[16];
     const uint32_t t = threadIdx.x, b = blockIdx.x;
-    // sum of the blocks before this one
-    uint64_t p = 0;
+    // sum of the blocks before this one (plus the carried base of the frames before the range)
+    uint64_t p = (base && t == 0) ? *base : 0;
     for (uint32_t j = t; j < b; j += 1024u) p += part[j];
     uint64_t before;
     (void)block_excl_scan(p, bsum, &before);
@@ -722,16 +722,19 @@ hipError_t launch_frame_totals(const EncodeArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// part: ceil(n / 4096) u64 of scratch (NULL: the one-workgroup k_scan)
+// part: ceil(n / 4096) u64 of scratch (NULL: the one-workgroup k_scan).  base (multi-workgroup
+// form only): a device u64 added to every offset -- the bytes of the frames before the range,
+// for a call scanned range by range (overlapped encode, fg_api.cpp)
 hipError_t launch_scan(const uint32_t *sizes, uint64_t *offsets, uint64_t *total, uint32_t n, uint64_t *part,
-                       hipStream_t st) {
+                       hipStream_t st, const uint64_t *base) {
+    if (base && !part) return hipErrorInvalidValue;
     if (!part) {
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, sizes, offsets, total, n);
         return hipGetLastError();
     }
     const uint32_t nb = (n + kScanBlock - 1u) / kScanBlock;
     if (nb > 1u) hipLaunchKernelGGL(k_scan_part, dim3(nb), dim3(1024), 0, st, sizes, part, n);
-    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, sizes, offsets, total, part, n);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, sizes, offsets, total, part, n, base);
     return hipGetLastError();
 }
 

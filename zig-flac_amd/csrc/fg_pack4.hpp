@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
     const bool stereo = a.stereo != 0;
 
     uint32_t *ctr = a.work_ctr + 2u;
-    if (blockIdx.x == 0 && tid == 0) a.work_ctr[0] = a.work_ctr[1] = 0u;  // the analysis kernel's queues
+    reset_analysis_tickets(a.work_ctr, tid);  // the analysis kernel's queues
     if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
     __syncthreads();
     uint32_t jidx = blockIdx.x, buf = 0;

@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     const bool stereo = a.stereo != 0;
 
     uint32_t *ctr = a.work_ctr + 2u;
-    if (blockIdx.x == 0 && tid == 0) a.work_ctr[0] = a.work_ctr[1] = 0u;  // the analysis kernel's queues
+    reset_analysis_tickets(a.work_ctr, tid);  // the analysis kernel's queues
     if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
     __syncthreads();
     const uint32_t n_items = a.n_jobs << ssh;

@@ -213,6 +213,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_kernel_time": (I32, [P, I32, ctypes.POINTER(U64), ctypes.POINTER(ctypes.c_double)]),
         "flacgpu_reset_timing": (I32, [P]),
         "flacgpu_set_records": (I32, [P, I32]),
+        "flacgpu_set_overlap": (I32, [P, U32, U32, U32, U32]),
         "flacgpu_get_records": (I32, [P, P, U64, ctypes.POINTER(U64)]),
         "flacgpu_get_config": (I32, [P, ctypes.POINTER(Config)]),
         "flacgpu_wav_parse": (I32, [P, SZ, ctypes.POINTER(WavInfo)]),
@@ -246,7 +247,7 @@ def exported_symbols() -> list:
         "flacgpu_streaminfo_replay_device",
         "flacgpu_md5_set_engine", "flacgpu_md5_get_engine", "flacgpu_md5_state_init",
         "flacgpu_set_timing",
-        "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_get_records",
+        "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_set_overlap", "flacgpu_get_records",
         "flacgpu_get_config", "flacgpu_wav_parse", "flacgpu_streaminfo_init", "flacgpu_streaminfo_update_frame_size",
         "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file",
         "flacgpu_wav_to_flac", "flacgpu_open_multi", "flacgpu_close_multi", "flacgpu_multi_encode_frames",
@@ -491,6 +492,11 @@ class Encoder:
         ms = ctypes.c_double(0)
         _check(self.lib.flacgpu_kernel_time(self.ctx, k, ctypes.byref(n), ctypes.byref(ms)), "kernel_time")
         return n.value, ms.value
+
+    def set_overlap(self, ranges: int, ana_per_cu: int = 2, pack_per_cu: int = 2, min_frames: int = 4096) -> None:
+        """Encode schedule (flacgpu_set_overlap): ranges > 1 overlaps the analysis of range i+1 with the
+        scan + pack of range i on a second HIP stream; output bytes are unchanged."""
+        _check(self.lib.flacgpu_set_overlap(self.ctx, ranges, ana_per_cu, pack_per_cu, min_frames), "set_overlap")
 
     def set_records(self, on: bool) -> None:
         _check(self.lib.flacgpu_set_records(self.ctx, 1 if on else 0), "set_records")
