@@ -64,6 +64,13 @@ uint32_t crc_zpow(uint64_t e) {
     return result;
 }
 
+// z^e mod Q, Q = z^15 + z + 1 (a factor of P): the shift constants of the table-free CRC fold
+// (fg_device.hpp crc_lane_q)
+uint32_t q_zpow(uint64_t e) {
+    const uint32_t r = crc_zpow(e);
+    return (r & 0x8000u) ? r ^ 0x8003u : r;
+}
+
 struct TimedLaunch {
     int kernel;
     hipEvent_t start, stop;
@@ -82,7 +89,7 @@ struct flacgpu_ctx {
     hipStream_t stream = nullptr, aux = nullptr;
     hipStream_t dl = nullptr;  // download stream of the pipelined host-buffer path
     hipEvent_t fork = nullptr, join = nullptr;
-    uint16_t *d_crc_tab = nullptr, *d_crc_pow = nullptr, *d_crc_join = nullptr, *d_crc_pow4 = nullptr;
+    uint16_t *d_crc_pow = nullptr, *d_crc_join = nullptr, *d_crc_pow4 = nullptr;
     // full 16-bit two-channel frames are packed by k_pack4 (four waves per subframe): 512 threads
     uint32_t nt_pack4 = 0, lds_pack4 = 0, crc_hmax4 = 0;
     uint32_t *d_err = nullptr, *d_ctr = nullptr;
@@ -277,7 +284,6 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.out_cap = out_cap;
     a.err = c->d_err;
     a.work_ctr = c->d_ctr;
-    a.crc_tab = c->d_crc_tab;
     a.crc_pow = c->d_crc_pow;
     a.crc_pow4 = c->d_crc_pow4;
     a.crc_hmax4 = c->crc_hmax4;
@@ -639,27 +645,23 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
 
-    // CRC-16 tables: x * z^e mod P for e = 40, 32, 24, 16, 72, 64, 56, 48 (crc_word / crc_word2)
-    std::vector<uint16_t> tab(2048);
-    const uint32_t ze[8] = {crc_zpow(40), crc_zpow(32), crc_zpow(24), crc_zpow(16),
-                            crc_zpow(72), crc_zpow(64), crc_zpow(56), crc_zpow(48)};
-    for (int t = 0; t < 8; t++)
-        for (uint32_t x = 0; x < 256; x++) tab[t * 256 + x] = (uint16_t)crc_mulmod_host(x, ze[t]);
+    // CRC-16 shift constants of the table-free fold (mod Q, fg_device.hpp crc_lane_q): thread t
+    // of T folds 2H words, followed by 2H (T - 1 - t) words and the CRC's z^16
     const uint32_t T = c->nt_pack, HM = c->crc_hmax;
     std::vector<uint16_t> pw((size_t)HM * T), pj(HM);
     for (uint32_t h = 1; h <= HM; h++) {
-        pj[h - 1] = (uint16_t)crc_zpow(32ull * h);
-        for (uint32_t t = 0; t < T; t++) pw[(size_t)(h - 1) * T + t] = (uint16_t)crc_zpow(64ull * h * (T - 1u - t));
+        pj[h - 1] = (uint16_t)q_zpow(32ull * h);
+        for (uint32_t t = 0; t < T; t++) pw[(size_t)(h - 1) * T + t] = (uint16_t)q_zpow(16ull + 64ull * h * (T - 1u - t));
     }
-    const uint32_t T4 = c->nt_pack4, HM4 = c->crc_hmax4;  // HM4 <= HM: pj covers both
+    const uint32_t T4 = c->nt_pack4, HM4 = c->crc_hmax4;
     std::vector<uint16_t> pw4((size_t)HM4 * T4 + 1);
     for (uint32_t h = 1; h <= HM4; h++)
-        for (uint32_t t = 0; t < T4; t++) pw4[(size_t)(h - 1) * T4 + t] = (uint16_t)crc_zpow(64ull * h * (T4 - 1u - t));
+        for (uint32_t t = 0; t < T4; t++) pw4[(size_t)(h - 1) * T4 + t] = (uint16_t)q_zpow(16ull + 64ull * h * (T4 - 1u - t));
 
     std::vector<uint16_t> pws((size_t)c->crc_hmaxs * c->nt_psplit + 1), x8(24);
     for (uint32_t h = 1; h <= c->crc_hmaxs; h++)
         for (uint32_t t = 0; t < c->nt_psplit; t++)
-            pws[(size_t)(h - 1) * c->nt_psplit + t] = (uint16_t)crc_zpow(64ull * h * (c->nt_psplit - 1u - t));
+            pws[(size_t)(h - 1) * c->nt_psplit + t] = (uint16_t)q_zpow(16ull + 64ull * h * (c->nt_psplit - 1u - t));
     for (uint32_t i = 0; i < 24; i++) x8[i] = (uint16_t)crc_zpow(8ull << i);
     if (hipMalloc(&c->d_crc_pows, pws.size() * 2) || hipMalloc(&c->d_crc_x8, 48) ||
         hipMemcpy(c->d_crc_pows, pws.data(), pws.size() * 2, hipMemcpyHostToDevice) ||
@@ -669,7 +671,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     const uint64_t F = c->max_frames;
     c->pcm_cap = F * (uint64_t)kBlock * c->C * c->B + 64;
     c->out_cap = F * (uint64_t)c->image_bytes;
-    if (hipMalloc(&c->d_crc_tab, 2048 * 2) || hipMalloc(&c->d_crc_pow, pw.size() * 2) ||
+    if (hipMalloc(&c->d_crc_pow, pw.size() * 2) ||
         hipMalloc(&c->d_crc_pow4, pw4.size() * 2) ||
         hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) || hipMalloc(&c->d_ctr, 4u * kCtrSet * kOvlMaxChunks) ||
         hipMalloc(&c->d_cum, 8u * (kOvlMaxChunks + 1u)) ||
@@ -677,8 +679,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
         hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16) || hipMalloc(&c->d_stamps, 32 * 8))
         return fail(FLACGPU_ERR_OUT_OF_MEMORY);
-    if (hipMemcpy(c->d_crc_tab, tab.data(), 4096, hipMemcpyHostToDevice) ||
-        hipMemcpy(c->d_crc_pow, pw.data(), pw.size() * 2, hipMemcpyHostToDevice) ||
+    if (hipMemcpy(c->d_crc_pow, pw.data(), pw.size() * 2, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_pow4, pw4.data(), pw4.size() * 2, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_crc_join, pj.data(), pj.size() * 2, hipMemcpyHostToDevice) || hipMemset(c->d_err, 0, 16) || hipMemset(c->d_ctr, 0, 4u * kCtrSet * kOvlMaxChunks) ||
         hipMemset(c->d_stamps, 0, 32 * 8))
@@ -694,7 +695,6 @@ void flacgpu_close(flacgpu_ctx *c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     resolve_timing(c);
     for (auto e : c->event_pool) hipEventDestroy(e);
-    hipFree(c->d_crc_tab);
     hipFree(c->d_crc_pow);
     hipFree(c->d_crc_pow4);
     hipFree(c->d_crc_join);

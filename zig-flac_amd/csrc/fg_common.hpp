@@ -126,9 +126,8 @@ struct EncodeArgs {
     uint32_t *work_ctr;         // kCtrSet frame-queue tickets: analysis full/tail, pack full/tail,
                                 // per-XCD split-analysis queues (each stage zeroes the other's)
     uint32_t *err;              // device error word (0 = ok; bit 0 invariant, bit 1 output too small)
-    const uint16_t *crc_tab;    // 8 x 256: z^40, z^32, z^24, z^16, z^72, z^64, z^56, z^48 byte tables (CRC-16/UMTS)
-    const uint16_t *crc_pow;    // [(H-1)*pack_threads + t] = z^(64*H*(T-1-t)) mod P, H = 1..crc_hmax
-    const uint16_t *crc_join;   // [H-1] = z^(32*H)
+    const uint16_t *crc_pow;    // [(H-1)*pack_threads + t] = z^(16+64*H*(T-1-t)) mod Q (Q = z^15+z+1), H = 1..crc_hmax
+    const uint16_t *crc_join;   // [H-1] = z^(32*H) mod Q
     uint32_t crc_hmax;          // largest half-segment (words) of the CRC fold
     const uint16_t *crc_pow4;   // the same for the four-waves-per-subframe pack kernel (k_pack4, 512 threads)
     uint32_t crc_hmax4;

@@ -218,29 +218,51 @@ __device__ __forceinline__ uint32_t rice_choose(uint32_t S, uint32_t len, uint32
     return 0x80u | width;
 }
 
-// CRC-16/UMTS helpers (crc16.zig; poly 0x8005, init 0).  tab = 4 x 256 u16:
-// [0] x*z^40, [1] x*z^32, [2] x*z^24, [3] x*z^16 (mod P).  W is a stream word
-// whose first byte sits in bits 31..24.
-__device__ __forceinline__ uint32_t crc_word(uint32_t crc, uint32_t W, const uint16_t *tab) {
-    const uint32_t X = W ^ (crc << 16);
-    return (uint32_t)tab[X >> 24] ^ (uint32_t)tab[256 + ((X >> 16) & 255u)] ^
-           (uint32_t)tab[512 + ((X >> 8) & 255u)] ^ (uint32_t)tab[768 + (X & 255u)];
+// CRC-16/UMTS (crc16.zig: poly 0x8005, init 0) without tables.  P = z^16 + z^15 + z^2 + 1 = (z + 1)(z^15 + z + 1), so a residue
+// mod P is the pair (residue mod Q = z^15 + z + 1, residue mod z + 1 = the parity of the
+// message bits), recombined by CRT: r = A ^ (parity(A) != p ? Q : 0) (Q has three terms, so
+// adding it flips the parity and keeps A mod Q).  Mod Q, z^15 = z + 1 folds 14 bits per
+// shift/XOR step, so the per-lane CRC chain is VALU only -- no table gathers, whose random
+// indices cost 2-3 LDS bank-conflict cycles each.  Frame words are big-endian (first byte in bits
+// 31..24), so a word is the next 32 coefficients of the message polynomial.
+__device__ __forceinline__ uint32_t q_fold(uint32_t t) {  // t < 2^32 -> same residue, < 2^18
+    const uint32_t h = t >> 15;
+    return (t & 0x7FFFu) ^ h ^ (h << 1);
 }
-__device__ __forceinline__ uint32_t crc_byte(uint32_t crc, uint32_t b, const uint16_t *tab) {
-    return ((crc << 8) & 0xFFFFu) ^ (uint32_t)tab[768 + (((crc >> 8) ^ b) & 255u)];
+// s * z^32 + W mod Q (z^32 = z^4 + z^2 mod Q); s < 2^18 in and out, not fully reduced
+__device__ __forceinline__ uint32_t q_word(uint32_t s, uint32_t W) { return q_fold(W ^ (s << 4) ^ (s << 2)); }
+// a * e mod Q, a and e < 2^15 (fully reduced): 15 terms accumulated in one register (once per
+// frame per lane: few live registers matter more than the chain), one fold
+__device__ __forceinline__ uint32_t q_mul(uint32_t a, uint32_t e) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 15; i++) r ^= (e << i) & (uint32_t)(-(int32_t)((a >> i) & 1u));
+    return q_fold(r);
 }
-// Eight bytes per step (two stream words): only W0's bytes depend on the running CRC, so the
-// four lookups of W1 issue ahead of it.  tab[1024..2047] = z^72, z^64, z^56, z^48.
-__device__ __forceinline__ uint32_t crc_word2(uint32_t crc, uint32_t W0, uint32_t W1, const uint16_t *tab) {
-    const uint32_t X = W0 ^ (crc << 16);
-    return (uint32_t)tab[1024 + (X >> 24)] ^ (uint32_t)tab[1280 + ((X >> 16) & 255u)] ^
-           (uint32_t)tab[1536 + ((X >> 8) & 255u)] ^ (uint32_t)tab[1792 + (X & 255u)] ^ (uint32_t)tab[W1 >> 24] ^
-           (uint32_t)tab[256 + ((W1 >> 16) & 255u)] ^ (uint32_t)tab[512 + ((W1 >> 8) & 255u)] ^
-           (uint32_t)tab[768 + (W1 & 255u)];
+// (residue mod Q in bits 0..14, message parity in bit 16) -> CRC-16 register value
+__device__ __forceinline__ uint32_t crc_from_q(uint32_t qp) {
+    const uint32_t A = qp & 0x7FFFu;
+    return A ^ (((__builtin_popcount(A) ^ (qp >> 16)) & 1u) ? 0x8003u : 0u);
 }
-// a(z) * b(z) mod P: the 31-bit carry-less product as a balanced XOR of 16 independent
-// terms (no serial bit loop), its top 15 bits folded back through the z^16 / z^24 tables.
-__device__ __forceinline__ uint32_t crc_mulmod_t(uint32_t a, uint32_t b, const uint16_t *tab) {
+// one lane's share of a frame CRC: words [va, va + n) of img (negative indices read as zero: the
+// front padding of an init-0 CRC), times e = z^(16 + 32 * words after them) mod Q; parity in bit 16.
+__device__ __forceinline__ uint32_t crc_lane_q(const uint32_t *img, int32_t va, uint32_t n, uint32_t e) {
+    uint32_t s = 0, px = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const int32_t r = va + (int32_t)i;
+        const uint32_t w = r >= 0 ? img[r] : 0u;
+        s = q_word(s, w);
+        px ^= w;
+    }
+    return q_mul(q_fold(s), e) | ((__builtin_popcount(px) & 1u) << 16);
+}
+// crc16.zig's byte step without a table: T[t] = t * z^16 mod P = (t << 1) ^ (t << 2) ^ (parity(t) ? Q : 0)
+__device__ __forceinline__ uint32_t crc_byte_v(uint32_t crc, uint32_t b) {
+    const uint32_t t = ((crc >> 8) ^ b) & 255u;
+    return ((crc << 8) ^ (t << 1) ^ (t << 2) ^ ((__builtin_popcount(t) & 1u) ? 0x8003u : 0u)) & 0xFFFFu;
+}
+// a * b mod P for a, b < 2^16 without tables: the carry-less product mod Q plus its parity
+__device__ __forceinline__ uint32_t crc_mulmod_v(uint32_t a, uint32_t b) {
     uint32_t t[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) t[i] = (b << i) & (uint32_t)(-(int32_t)((a >> i) & 1u));
@@ -248,20 +270,7 @@ __device__ __forceinline__ uint32_t crc_mulmod_t(uint32_t a, uint32_t b, const u
     for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
         for (int i = 0; i < w; i++) t[i] ^= t[i + w];
-    const uint32_t hi = t[0] >> 16;
-    return (t[0] & 0xFFFFu) ^ (uint32_t)tab[768 + (hi & 255u)] ^ (uint32_t)tab[512 + (hi >> 8)];
-}
-
-// a(z) * b(z) mod (z^16 + z^15 + z^2 + 1)
-__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int i = 15; i >= 0; i--) {
-        r <<= 1;
-        r ^= (r & 0x10000u) ? 0x18005u : 0u;
-        r ^= ((a >> i) & 1u) ? b : 0u;
-    }
-    return r & 0xFFFFu;
+    return crc_from_q(q_fold(q_fold(t[0])) | ((__builtin_popcount(t[0]) & 1u) << 16));
 }
 
 // OR two words into LDS at byte address addr (4-aligned) and addr + 4.  Inline asm: the
@@ -280,14 +289,25 @@ __device__ __forceinline__ void store_frame16(const uint32_t *img, uint8_t *out,
     const uint32_t sa = (uint32_t)(D & 3u);
     const uint64_t qD = D >> 2;
     const uint64_t DL = D + lo;
+    // the unit's image words m0 - 1 .. m0 + 3 lie in the two 16-B-aligned blocks at m0 + r - 4 and
+    // m0 + r (r = qD & 3, uniform): two conflict-free ds_read_b128 per unit instead of five
+    // ds_read_b32 at a 4-word lane stride (4-way bank conflicts)
+    const uint32_t r = (uint32_t)(qD & 3u);
     for (uint64_t u = (DL >> 4) + tid; u < ((E + 15u) >> 4); u += NT) {
         const int32_t m0 = (int32_t)(4u * u - qD);  // image word of the unit's first word (>= -3)
+        const int32_t a1 = m0 + (int32_t)r;           // >= 0, a multiple of 4
+        const uint4 q1 = *(const uint4 *)(img + a1);
+        const uint4 q0 = a1 >= 4 ? *(const uint4 *)(img + a1 - 4) : make_uint4(0, 0, 0, 0);
+        const uint32_t w8[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        uint32_t wv[5];  // image words m0 - 1 .. m0 + 3 = w8[3 - r .. 7 - r]
+#pragma unroll
+        for (int c = 0; c < 5; c++)
+            wv[c] = r == 0 ? w8[3 + c] : r == 1 ? w8[2 + c] : r == 2 ? w8[1 + c] : w8[c];
         uint32_t v[4];
-        uint32_t prev = m0 >= 1 ? img[m0 - 1] : 0u;
+        uint32_t prev = m0 >= 1 ? wv[0] : 0u;
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            const int32_t m = m0 + c;
-            const uint32_t lo = m >= 0 ? img[m] : 0u;
+            const uint32_t lo = m0 + c >= 0 ? wv[c + 1] : 0u;
             v[c] = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(prev, lo, sa) : lo);
             prev = lo;
         }
@@ -2080,9 +2100,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
     const uint32_t cst = cw + stage_pad(C, B);
     const bool dbuf = FULL && a.pack_dbuf != 0;
     const PackLayout LY = pack_layout(C, B, a.image_bytes, dbuf);
-    uint16_t *crct = (uint16_t *)(smem + LY.crc);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
-    for (uint32_t i = tid; i < 2048u; i += NT) crct[i] = a.crc_tab[i];
     const bool stereo = a.stereo != 0;
 
     // Persistent loop over a dynamic frame queue, two frames ahead: while frame i is packed, the
@@ -2354,33 +2372,32 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         STAMP(4);
         // ---- 4. CRC-16 of the frame: the word stream is front-padded with zero words (a no-op
         // for an init-0 CRC) to NT*2H words; thread t folds its 2H words as two interleaved
-        // halves, joins them (x z^(32H)), shifts by z^(64H(NT-1-t)) and the workgroup
-        // XOR-reduces.  H is odd so the per-thread word stride 2H costs at most 2-way conflicts.
+        // halves in table-free chains mod Q (crc_lane_q), joins them (x z^(32H) mod Q), scales by
+        // z^(16 + 64H(NT-1-t)) mod Q and the workgroup XOR-reduces residue and parity.  H is odd so
+        // the per-thread word stride 2H costs at most 2-way conflicts.
         {
-            // two interleaved halves of H words per thread, eight bytes per step (H odd: one
-            // four-byte step at the end); words before the stream start read as zero
             const int32_t Z = (int32_t)(NT * 2u * H) - (int32_t)W4;
-            uint32_t ca = 0, cb = 0;
             const int32_t va = (int32_t)(tid * 2u * H) - Z, vb = va + (int32_t)H;
-            auto word = [&](int32_t r) -> uint32_t { return r >= 0 ? img[r] : 0u; };
-            uint32_t i = 0;
-            for (; i + 1u < H; i += 2u) {
-                ca = crc_word2(ca, word(va + (int32_t)i), word(va + (int32_t)i + 1), crct);
-                cb = crc_word2(cb, word(vb + (int32_t)i), word(vb + (int32_t)i + 1), crct);
+            uint32_t sa = 0, sb = 0, px = 0;
+            for (uint32_t i = 0; i < H; i++) {
+                const int32_t ra = va + (int32_t)i, rb = vb + (int32_t)i;
+                const uint32_t wa = ra >= 0 ? img[ra] : 0u, wb = rb >= 0 ? img[rb] : 0u;
+                sa = q_word(sa, wa);
+                sb = q_word(sb, wb);
+                px ^= wa ^ wb;
             }
-            ca = crc_word(ca, word(va + (int32_t)i), crct);
-            cb = crc_word(cb, word(vb + (int32_t)i), crct);
-            const uint32_t ct = crc_mulmod_t(ca, crc_jw, crct) ^ cb;
-            uint32_t contrib = crc_mulmod_t(ct, crc_pw, crct);
+            const uint32_t ct = q_fold(q_mul(q_fold(sa), crc_jw) ^ sb);
+            uint32_t contrib = q_mul(ct, crc_pw) | ((__builtin_popcount(px) & 1u) << 16);
             contrib = wave_xor32(contrib);
             if (l == 0) misc[wave] = contrib;
         }
         __syncthreads();
         if (tid == 0) {
-            uint32_t crc = 0;
-            for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
+            uint32_t qp = 0;
+            for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
+            uint32_t crc = crc_from_q(qp);
             for (uint32_t b = W4 * 4u; b < Lb; b++)
-                crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+                crc = crc_byte_v(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u);
             put_bits(img, Lb * 8u, crc, 16);
         }
         __syncthreads();

@@ -52,9 +52,7 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l0 = lane_id();
     const uint32_t sfi = wave >> 2, qw = wave & 3u;  // written subframe, quarter
     const PackLayout LY = pack_layout(C, B, a.image_bytes, true);
-    uint16_t *crct = (uint16_t *)(smem + LY.crc);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
-    for (uint32_t i = tid; i < 2048u; i += NT) crct[i] = a.crc_tab[i];
     const bool stereo = a.stereo != 0;
 
     uint32_t *ctr = a.work_ctr + 2u;
@@ -296,25 +294,23 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         STAMP(4);
 
         // ---- 4. CRC-16 of the frame: the word stream front-padded with zero words (a no-op for
-        // an init-0 CRC) to NT * 2H words; thread t folds its 2H words in one chain, eight bytes
-        // per step, and shifts the result by z^(64H(NT-1-t)); the workgroup XOR-reduces.
+        // an init-0 CRC) to NT * 2H words; thread t folds its 2H words in one table-free chain mod
+        // Q (crc_lane_q) scaled by z^(16 + 64H(NT-1-t)) mod Q, with its words' parity; the
+        // workgroup XOR-reduces both and thread 0 recombines them into the CRC (crc_from_q).
         {
             const int32_t Z = (int32_t)(NT * 2u * H) - (int32_t)W4;
-            uint32_t ca = 0;
             const int32_t va = (int32_t)(tid * 2u * H) - Z;
-            auto word = [&](int32_t rr) -> uint32_t { return rr >= 0 ? img[rr] : 0u; };
-            for (uint32_t i = 0; i < 2u * H; i += 2u)
-                ca = crc_word2(ca, word(va + (int32_t)i), word(va + (int32_t)i + 1), crct);
-            uint32_t contrib = crc_mulmod_t(ca, crc_pw, crct);
+            uint32_t contrib = crc_lane_q(img, va, 2u * H, crc_pw);
             contrib = wave_xor32(contrib);
             if (l == 0) misc[wave] = contrib;
         }
         bar_lds();
         if (tid == 0) {
-            uint32_t crc = 0;
-            for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
+            uint32_t qp = 0;
+            for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
+            uint32_t crc = crc_from_q(qp);
             for (uint32_t b = W4 * 4u; b < Lb; b++)
-                crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+                crc = crc_byte_v(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u);
             put_bits(img, Lb * 8u, crc, 16);
         }
         bar_lds();

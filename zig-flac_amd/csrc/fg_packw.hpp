@@ -72,10 +72,10 @@ __device__ __forceinline__ void stage_dma_w(const uint8_t *pcm, uint64_t off, ui
 
 // z^(8 m) mod P for m < 2^24, wave-parallel: lane i < 24 contributes z^(8 * 2^i) when bit i of
 // m is set, the 32-lane product by a butterfly of table-assisted carry-less multiplies
-__device__ __forceinline__ uint32_t crc_zpow8(uint32_t m, const uint16_t *x8, const uint16_t *crct, uint32_t l) {
+__device__ __forceinline__ uint32_t crc_zpow8(uint32_t m, const uint16_t *x8, uint32_t l) {
     uint32_t f = (l < 24u && ((m >> l) & 1u)) ? (uint32_t)x8[l] : 1u;
 #pragma unroll
-    for (int d = 1; d < 32; d <<= 1) f = crc_mulmod_t(f, (uint32_t)__shfl_xor((int)f, d), crct);
+    for (int d = 1; d < 32; d <<= 1) f = crc_mulmod_v(f, (uint32_t)__shfl_xor((int)f, d));
     return f;
 }
 
@@ -115,9 +115,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         const uint32_t k = 64u * xi + l0, sub = k / (sw + 1u), o = k - sub * (sw + 1u);
         dcode |= (((o == sw || k >= cst) ? 4u : 0u) | (sub & 3u)) << (3u * xi);
     }
-    uint16_t *crct = (uint16_t *)(smem + LY.crc);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
-    for (uint32_t i = tid; i < 2048u; i += NT) crct[i] = a.crc_tab[i];
     const bool stereo = a.stereo != 0;
 
     uint32_t *ctr = a.work_ctr + 2u;
@@ -427,25 +425,22 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         bar_lds();
         STAMP(4);
 
-        // ---- 4. CRC-16 of the frame (one chain of 2H words per thread, see k_pack4)
+        // ---- 4. CRC-16 of the frame (one table-free chain of 2H words per thread, see k_pack4)
         {
             const int32_t Z = (int32_t)(NT * 2u * H) - (int32_t)W4;
-            uint32_t ca = 0;
             const int32_t va = (int32_t)(tid * 2u * H) - Z;
-            auto word = [&](int32_t rr) -> uint32_t { return rr >= 0 ? img[rr] : 0u; };
-            for (uint32_t i = 0; i < 2u * H; i += 2u)
-                ca = crc_word2(ca, word(va + (int32_t)i), word(va + (int32_t)i + 1), crct);
-            uint32_t contrib = crc_mulmod_t(ca, crc_pw, crct);
+            uint32_t contrib = crc_lane_q(img, va, 2u * H, crc_pw);
             contrib = wave_xor32(contrib);
             if (l == 0) misc[wave] = contrib;
         }
         bar_lds();
         if (!SPLIT) {
             if (tid == 0) {
-                uint32_t crc = 0;
-                for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
+                uint32_t qp = 0;
+                for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
+                uint32_t crc = crc_from_q(qp);
                 for (uint32_t b = W4 * 4u; b < Lb; b++)
-                    crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+                    crc = crc_byte_v(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u);
                 put_bits(img, Lb * 8u, crc, 16);
             }
             bar_lds();
@@ -455,13 +450,14 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             store_frame16(img, a.out, D, fbytes, tid, NT);
         } else if (wave == 0) {
             // ---- 4b. this half's CRC partial (half 0: shifted past the bytes after its image)
-            uint32_t crc = 0;
-            for (uint32_t i = 0; i < NW; i++) crc ^= misc[i];
+            uint32_t qp = 0;
+            for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
+            uint32_t crc = crc_from_q(qp);
             if (l == 0)
                 for (uint32_t b = W4 * 4u; b < Lb; b++)
-                    crc = crc_byte(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u, crct);
+                    crc = crc_byte_v(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u);
             crc = (uint32_t)__shfl((int)crc, 0);
-            if (half == 0) crc = crc_mulmod_t(crc, crc_zpow8(Lt - Lb, a.crc_x8, crct, l), crct);
+            if (half == 0) crc = crc_mulmod_v(crc, crc_zpow8(Lt - Lb, a.crc_x8, l));
             const bool shared = (b0 & 7u) != 0;  // one byte holds bits of both halves
             const uint32_t sb = shared ? (half ? img[0] >> 24 : (img[(Lb - 1u) >> 2] >> (24 - 8 * ((Lb - 1u) & 3))) & 255u)
                                        : 0u;
