@@ -608,7 +608,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         c->pack_dbuf = packw_dbuf;  // k_pack then runs tail frames only (never double-buffered)
     }
     if (c->nt_pack4) {
-        c->lds_pack4 = (c->C == 2 && c->B == 2 && !lpc) ? pack_layout(c->C, c->B, c->image_bytes, true).total
+        c->lds_pack4 = (c->C == 2 && c->B == 2 && !lpc) ? pack4_layout(c->image_bytes).total
                                                          : packw_layout(c->C, c->B, c->nt_pack4 / (64u * n_out), c->image_bytes, packw_dbuf).total;
         c->crc_hmax4 = ((c->image_bytes / 4u + 2u * c->nt_pack4 - 1u) / (2u * c->nt_pack4)) | 1u;
     }

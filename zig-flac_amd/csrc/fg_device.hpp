@@ -510,6 +510,35 @@ struct CandRes {
     } while (0)
 #endif
 
+// LDS-DMA (global_load_lds_dword / _dwordx4) issued from inline asm.  Issued through the
+// builtin, the compiler's wait-count pass cannot tell the DMA's LDS destination from the LDS
+// the kernel reads next (one extern array), so it put an s_waitcnt vmcnt(0) before the first
+// LDS access after every DMA: each wave waited for the next frame's PCM right after issuing it,
+// and the double-buffered prefetch hid nothing.  Hidden from that pass, the DMA is waited for
+// only where the kernels say so (an explicit s_waitcnt vmcnt before the data is read); the
+// compiler's own vmcnt waits stay correct, only conservative (in-order completion).  M0 (the
+// LDS base of the wave's piece) is saved and restored around the instruction.
+#ifndef FG_DMA_ASM
+#define FG_DMA_ASM 1
+#endif
+template <int SZ>
+__device__ __forceinline__ void lds_dma(const void *g, void *lds) {
+#if FG_DMA_ASM
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)lds);
+    uint32_t sv;
+    if constexpr (SZ == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(sv) : "s"(m), "v"(g) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(sv) : "s"(m), "v"(g) : "memory");
+#else
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)lds, SZ, 0, 0);
+#endif
+}
+
 // LDS-DMA one full frame into the staging area.  Interleaved 16-bit stereo layout
 // (fg_layout.hpp): 16 instructions of 1 KiB, lane i of instruction k filling byte 16i of
 // block k from 16-B group i >> 2 of chunk 4k + (i & 3).  Padded layouts: each
@@ -522,9 +551,7 @@ __device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint
     const uint32_t *src = (const uint32_t *)(pcm + off);
     if (ilv) {
         for (uint32_t k = wave; k < 16u; k += NW)
-            __builtin_amdgcn_global_load_lds(
-                (__attribute__((address_space(1))) void *)(src + (4u * k + (l & 3u)) * 64u + 4u * (l >> 2)),
-                (__attribute__((address_space(3))) void *)(stg + 272u * k), 16, 0, 0);
+            lds_dma<16>(src + (4u * k + (l & 3u)) * 64u + 4u * (l >> 2), stg + 272u * k);
         return;
     }
     if (drh) {
@@ -533,9 +560,7 @@ __device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint
             for (uint32_t x0 = 0; x0 < cw; x0 += 64u) {
                 const uint32_t x = x0 + l, r = (uint32_t)((float)x * inv), k = x - r * drh;
                 if (x < cw)
-                    __builtin_amdgcn_global_load_lds(
-                        (__attribute__((address_space(1))) void *)(src + ch * 2u * cw + r * 2u * drh + half * drh + k),
-                        (__attribute__((address_space(3))) void *)(stg + ch * cst + x0), 4, 0, 0);
+                    lds_dma<4>(src + ch * 2u * cw + r * 2u * drh + half * drh + k, stg + ch * cst + x0);
             }
         }
         return;
@@ -543,13 +568,15 @@ __device__ __forceinline__ void stage_dma(const uint8_t *pcm, uint64_t off, uint
     for (uint32_t ch = wave; ch < 64u; ch += NW) {
         for (uint32_t x0 = 0; x0 < cw; x0 += 64u) {
             if (x0 + l < cw)
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + ch * cw + x0 + l),
-                                                 (__attribute__((address_space(3))) void *)(stg + ch * cst + x0), 4,
-                                                 0, 0);
+                lds_dma<4>(src + ch * cw + x0 + l, stg + ch * cst + x0);
         }
     }
 }
 
+
+// Workgroup barrier for LDS hand-offs only: __syncthreads() would also wait for vmcnt(0),
+// i.e. drain the next frame's PCM DMA and this frame's output stores at every barrier.
+__device__ __forceinline__ void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Frame-queue tickets (EncodeArgs::work_ctr, one set of kCtrSet u32 per overlapped range):
 // [0] analysis full, [1] analysis tail, [2] pack full, [3] pack tail, [8..15] the split
@@ -1205,6 +1232,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     if (jidx < n_items) job = a.jobs[jidx >> ssh];
     if (nxt < n_items) jn = a.jobs[nxt >> ssh];
     if (dbuf && jidx < n_items) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0, NC == 2 && B == 2, drh, jidx & ssh);
+    // The ticket of the frame after next is taken at the END of the frame before (behind its
+    // descriptor stores, which the top of the next frame waits for anyway) and published at the
+    // estimate barrier (step 9).  Taken after the DMA of the next frame's PCM, the wait for the
+    // atomic's value also waited for that DMA.
+    uint32_t tk = 0;
+    if (tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
     while (jidx < n_items) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
         const uint32_t half = jidx & ssh;
@@ -1228,11 +1261,6 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         STAMP(10);
         if (dbuf && nxt < n_items)
             stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l, NC == 2 && B == 2, drh, nxt & ssh);
-        // The ticket of the frame after next is taken here, behind this frame's wait for its
-        // staged PCM, and its value is first used at the estimate barrier (step 9): taken at the
-        // top of the loop, the vmcnt(0) for the DMA also waited for the atomic's round trip.
-        uint32_t tk = 0;
-        if (tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
         STAMP(0);
 
         // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
@@ -1835,7 +1863,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             rc[6] = (uint32_t)R.est; rc[7] = (uint32_t)(R.est >> 32);
         }
         if (tid == 0) misc[20] = tk;
-        __syncthreads();
+        bar_lds();
         // the job record of the frame after next (DMA'd at the top of the next frame)
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         FrameJob jnn{};
@@ -2068,6 +2096,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // this frame's last reads before the next frame's writes; synchronous staging writes the
         // staging buffer before that barrier, so it needs its own
         if (!dbuf) __syncthreads();
+        if (tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
         STAMP(6);
         jidx = nxt; job = jn; nxt = nn; jn = jnn;
         buf ^= 1u;
@@ -2166,10 +2195,12 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         __syncthreads();
         STAMP(0);
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
-        if (dbuf && nxt < a.n_jobs)
-            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, wave, NW, l, NC == 2 && B == 2);
+        // the job record of the frame after next before the DMA: waiting for it then never
+        // waits for the DMA (vmcnt completes in order)
         FrameJob jnn{};
         if (nn < a.n_jobs) jnn = a.jobs[nn];
+        if (dbuf && nxt < a.n_jobs)
+            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, wave, NW, l, NC == 2 && B == 2);
         if (skip) {
             if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
             __syncthreads();
@@ -2181,15 +2212,17 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
         STAMP(9);
         // lane offsets from the measured segment lengths (uniform prefix of earlier subframes)
         const uint32_t seg = sd->lane_bits[l];
+        // subframes before this wave's: every subframe's bits in one load (lane t: subframe t)
+        const uint32_t sbits = l < NW ? ((const SubDesc *)(fd + sizeof(FrameDesc)) + l)->bits : 0u;
         uint32_t sub_start = 8u * F->hdr_bytes;
-        for (uint32_t t = 0; t < wave; t++) sub_start += ((const SubDesc *)(fd + sizeof(FrameDesc)) + t)->bits;
+        for (uint32_t t = 0; t < wave; t++) sub_start += rdl(sbits, (int)t);
         const uint32_t lane_off = wave_incl_scan32(seg) - seg;
         STAMP(10);
-        __syncthreads();  // staging dead: zero the image
+        bar_lds();  // staging dead: zero the image
         STAMP(1);
         const uint32_t Wz = (fbytes + 3u) / 4u + 2u;
         for (uint32_t i = tid; i < Wz; i += NT) img[i] = 0;
-        __syncthreads();
+        bar_lds();
         STAMP(2);
         if (tid < 4) {
             const uint32_t hv = F->hdr[tid];
@@ -2367,7 +2400,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
                 }
             }
         }
-        __syncthreads();
+        bar_lds();
 
         STAMP(4);
         // ---- 4. CRC-16 of the frame: the word stream is front-padded with zero words (a no-op
@@ -2391,7 +2424,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
             contrib = wave_xor32(contrib);
             if (l == 0) misc[wave] = contrib;
         }
-        __syncthreads();
+        bar_lds();
         if (tid == 0) {
             uint32_t qp = 0;
             for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
@@ -2400,7 +2433,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
                 crc = crc_byte_v(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u);
             put_bits(img, Lb * 8u, crc, 16);
         }
-        __syncthreads();
+        bar_lds();
 
         STAMP(5);
         // ---- 5. image -> out[D, D + fbytes)

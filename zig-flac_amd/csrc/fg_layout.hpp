@@ -90,6 +90,25 @@ __host__ __device__ inline PackLayout pack_layout(uint32_t C, uint32_t B, uint32
     return L;
 }
 
+// k_pack4 (fg_pack4.hpp): two staging / image buffers, scratch, and two LDS copies of a frame
+// descriptor (320 dwords each, DMA'd a frame ahead)
+struct P4Layout {
+    uint32_t buf0, buf1, misc, dsc0, dsc1, total;
+};
+__host__ __device__ inline P4Layout pack4_layout(uint32_t image_bytes) {
+    P4Layout L;
+    uint32_t r0 = stage_bytes(2, 2);
+    if (image_bytes > r0) r0 = image_bytes;
+    r0 = fg_round16(r0);
+    L.buf0 = 0;
+    L.buf1 = r0;
+    L.misc = 2u * r0;
+    L.dsc0 = L.misc + 256u;
+    L.dsc1 = L.dsc0 + 1280u;
+    L.total = fg_round16(L.dsc1 + 1280u);
+    return L;
+}
+
 // k_packw staging (fg_packw.hpp): 64 chunks of 64 samples, each split into WPS sub-chunks of
 // 64 / WPS samples (one lane's samples) followed by one pad word each, so the WPS lanes that read
 // one chunk start in different banks (with the plain pad they would all hit one: a sub-chunk of

@@ -23,9 +23,6 @@
 #define FG_PACK4_MINW 8
 #endif
 
-// Workgroup barrier for LDS hand-offs only: __syncthreads() would also wait for vmcnt(0),
-// i.e. drain the next frame's PCM DMA and this frame's output stores at every barrier.
-__device__ __forceinline__ void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // 16 instructions of 1 KiB: lane i of instruction k fills slot i & 3 of chunk 16k + (i >> 2)
 // from that chunk's 4-sample group ((i & 3) - (chunk >> 2)) & 3.
@@ -35,13 +32,40 @@ __device__ __forceinline__ void stage_dma_rot(const uint8_t *pcm, uint64_t off, 
     for (uint32_t k = wave; k < 16u; k += NW) {
         const uint32_t j = 16u * k + (l >> 2);
         const uint32_t g = ((l & 3u) - (j >> 2)) & 3u;
-        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + 16u * j + 4u * g),
-                                         (__attribute__((address_space(3))) void *)(stg + 256u * k), 16, 0, 0);
+        lds_dma<16>(src + 16u * j + 4u * g, stg + 256u * k);
     }
 }
 
 // dword offset of 4-sample group g of 16-sample chunk j in the rotated layout
 __device__ __forceinline__ uint32_t rot_off(uint32_t j, uint32_t g) { return 16u * j + 4u * ((g + (j >> 2)) & 3u); }
+
+// The frame descriptor in LDS (P4Layout dsc0 / dsc1, 320 dwords), DMA'd during the previous frame
+// together with the job record of the frame after it: [0..7] FrameDesc, [8..11] and [12..15] bytes
+// 0..15 of SubDesc 0 and 1 (type .. cand, lpc_shift, bits, lpc_prec), [16..17] the frame's byte
+// offset, [18..23] the next frame's FrameJob, [64..127] / [128..191] lane_bits of SubDesc 0 / 1,
+// [192..255] / [256..319] their Rice parameters.  Five 4-byte LDS-DMA instructions (waves 0..4).
+// Loaded at the top of their own frame, the two dependent round trips to the descriptor table
+// (written by the analysis kernel: an Infinity-Cache or HBM read) were 21 % of every pack wave's
+// time (r3g stamps), and the next job record's load waited behind the frame's PCM DMA.
+__device__ __forceinline__ void p4_dsc_dma(const EncodeArgs &a, uint32_t slot, uint32_t nxt_job, uint32_t *dsc,
+                                           uint32_t wave, uint32_t l) {
+    if (wave >= 5u) return;
+    const uint8_t *fd = a.desc + (uint64_t)slot * a.desc_stride;
+    const uint8_t *src;
+    if (wave == 0) {
+        if (l < 8u) src = fd + 4u * l;
+        else if (l < 12u) src = fd + 32u + 4u * (l - 8u);
+        else if (l < 16u) src = fd + 32u + sizeof(SubDesc) + 4u * (l - 12u);
+        else if (l < 18u) src = (const uint8_t *)(a.offsets + slot) + 4u * (l - 16u);
+        else if (l < 24u && nxt_job < a.n_jobs) src = (const uint8_t *)(a.jobs + nxt_job) + 4u * (l - 18u);
+        else src = fd;
+    } else if (wave <= 2u) {
+        src = fd + 32u + (wave - 1u) * sizeof(SubDesc) + offsetof(SubDesc, lane_bits) + 4u * l;
+    } else {
+        src = fd + 32u + (wave - 3u) * sizeof(SubDesc) + offsetof(SubDesc, params) + 4u * l;
+    }
+    lds_dma<4>(src, dsc + 64u * wave);
+}
 
 template <int MAXT>
 __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
@@ -51,64 +75,81 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
     const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6)), l0 = lane_id();
     const uint32_t sfi = wave >> 2, qw = wave & 3u;  // written subframe, quarter
-    const PackLayout LY = pack_layout(C, B, a.image_bytes, true);
+    const P4Layout LY = pack4_layout(a.image_bytes);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
     const bool stereo = a.stereo != 0;
 
+    // Tickets run two frames ahead.  The one for frame i+2 is taken at the END of frame i-1, after
+    // its output stores: the atomic's round trip then overlaps the wait for those stores that the
+    // top of frame i has anyway (taken after the DMAs of frame i, the wait for the atomic's value
+    // also waited for them), and it is published at the top of frame i.
     uint32_t *ctr = a.work_ctr + 2u;
     reset_analysis_tickets(a.work_ctr, tid);  // the analysis kernel's queues
     if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
     __syncthreads();
     uint32_t jidx = blockIdx.x, buf = 0;
     uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
-    FrameJob job{}, jn{};
-    if (jidx < a.n_jobs) job = a.jobs[jidx];
-    if (nxt < a.n_jobs) jn = a.jobs[nxt];
-    if (jidx < a.n_jobs) stage_dma_rot(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), wave, NW, l0);
+    uint32_t tk = 0;
+    if (tid == 0) tk = gridDim.x + atomicAdd(ctr, 1u);
+    uint32_t slot = 0;
+    if (jidx < a.n_jobs) {
+        const FrameJob job = a.jobs[jidx];
+        slot = job.slot;
+        stage_dma_rot(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), wave, NW, l0);
+        p4_dsc_dma(a, job.slot, nxt, (uint32_t *)(smem + LY.dsc0), wave, l0);
+    }
 #ifdef FG_STAMPS
     uint64_t ph_[16] = {};
     uint64_t tprev_ = __builtin_amdgcn_s_memtime();
 #endif
+    const uint32_t i0 = 1024u * qw + 16u * l0;  // first sample of this lane
     while (jidx < a.n_jobs) {
         const uint32_t l = opaque(l0);
-        if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
         uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
-        const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
-        const FrameDesc *F = (const FrameDesc *)fd;
-        const SubDesc *sd0 = (const SubDesc *)(fd + sizeof(FrameDesc));
-        const SubDesc *sd = sd0 + sfi;
-        const uint32_t total_bits = F->total_bits;
-        const uint32_t fbytes = ((total_bits + 7u) >> 3) + 2u;
-        const uint64_t D = a.offsets[job.slot];
-        const uint32_t Lb = (total_bits + 7u) >> 3;
-        const uint32_t W4 = Lb >> 2;
-        const uint32_t H = max((W4 + 2u * NT - 1u) / (2u * NT), 1u);  // words per thread / 2
-        const uint32_t hq = min(H, a.crc_hmax4) - 1u;
-        const uint32_t crc_pw = a.crc_pow4[hq * NT + tid];
-        const bool skip = fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap;  // uniform
-        const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
-                       method = sd->method, cand = sd->cand;
-        const uint32_t i0 = 1024u * qw + 16u * l0;  // first sample of this lane
-        const uint32_t p = sd->params[i0 >> (12u - o)];
-        const uint32_t lb = sd->lane_bits[l0];
-        uint32_t sub_start = 8u * F->hdr_bytes;
-        if (sfi) sub_start += sd0->bits;
+        const uint32_t *dsc = (const uint32_t *)(smem + (buf ? LY.dsc1 : LY.dsc0));
 
-        // ---- 1. PCM (DMA'd during the previous frame) -> this lane's samples and their history
+        // ---- 1. PCM and descriptor (DMA'd during the previous frame) -> this lane's samples
         STAMP(7);
+        if (tid == 0) misc[20] = tk;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP(8);
         __syncthreads();
         STAMP(0);
-        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
-        if (nxt < a.n_jobs) stage_dma_rot(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), wave, NW, l);
-        FrameJob jnn{};
-        if (nn < a.n_jobs) jnn = a.jobs[nn];
+        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);  // frame i+2
+        const uint32_t total_bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[1]);
+        const uint32_t fbytes = ((total_bits + 7u) >> 3) + 2u;
+        const uint64_t D = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[17]) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[16]);
+        const uint32_t Lb = (total_bits + 7u) >> 3;
+        const uint32_t W4 = Lb >> 2;
+        const uint32_t H = max((W4 + 2u * NT - 1u) / (2u * NT), 1u);  // words per thread / 2
+        const uint32_t hq = min(H, a.crc_hmax4) - 1u;
+        const bool skip = fbytes + 16u > a.image_bytes || D + fbytes > a.out_cap;  // uniform
+        const uint32_t sdw0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[8u + 4u * sfi]),
+                       sdw1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[9u + 4u * sfi]);
+        const uint32_t type = sdw0 & 255u, w = (sdw0 >> 8) & 255u, bd = (sdw0 >> 16) & 255u, k = sdw0 >> 24,
+                       o = sdw1 & 255u, method = (sdw1 >> 8) & 255u, cand = (sdw1 >> 16) & 255u;
+        const uint32_t p = ((const uint8_t *)(dsc + 192u + 64u * sfi))[i0 >> (12u - o)];
+        const uint32_t lb = dsc[64u + 64u * sfi + l];
+        uint32_t sub_start = 8u * (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[0]);
+        if (sfi) sub_start += (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[10]);
+        const uint32_t hdrw = dsc[4u + (l & 3u)];
+        const uint64_t jn_off = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[19]) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[18]);
+        const uint32_t jn_slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[23]);
+        const uint32_t crc_pw = a.crc_pow4[hq * NT + tid];   // first used in the CRC phase
+        if (nxt < a.n_jobs) {
+            stage_dma_rot(a.pcm, jn_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), wave, NW, l);
+            p4_dsc_dma(a, jn_slot, nn, (uint32_t *)(smem + (buf ? LY.dsc0 : LY.dsc1)), wave, l);
+        }
         if (skip) {
-            if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
+            if (tid == 0) {
+                atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
+                tk = gridDim.x + atomicAdd(ctr, 1u);
+            }
             __syncthreads();
-            jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= 1u;
+            jidx = nxt; nxt = nn; slot = jn_slot; buf ^= 1u;
             continue;
         }
         const uint32_t j = 64u * qw + l;  // this lane's 16-sample chunk
@@ -212,10 +253,7 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         const uint32_t lane_off = wave_incl_scan32(len) - len;
         bar_lds();  // image zeroed
         STAMP(3);
-        if (tid < 4) {
-            const uint32_t hv = F->hdr[tid];
-            if (hv) atomicOr(&img[tid], hv);
-        }
+        if (tid < 4 && hdrw) atomicOr(&img[tid], hdrw);
 
         // ---- 3. pack: each lane ORs its codes into the image at its bit offset
         {
@@ -226,6 +264,7 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
                 bw.init(img, pos);
                 if (type == 0) {  // writeConstantSubframe: 0x00, value << waste in bd bits
                     bw.put(0, 8);
+                    const SubDesc *sd = (const SubDesc *)(a.desc + (uint64_t)slot * a.desc_stride + sizeof(FrameDesc)) + sfi;
                     bw.put(((uint64_t)sd->cval << w) & (~0ull >> (64 - bd)), bd);
                 } else {
                     const uint32_t tc = (type == 1) ? 1u : (8u | k);
@@ -321,7 +360,8 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         // no barrier here: the image / staging area is next written by the DMA issued after the
         // next frame's top barrier, which already orders this frame's last reads before it
         STAMP(6);
-        jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= 1u;
+        if (tid == 0) tk = gridDim.x + atomicAdd(ctr, 1u);  // frame i+3, behind this frame's stores
+        jidx = nxt; nxt = nn; slot = jn_slot; buf ^= 1u;
     }  // persistent frame loop
 #ifdef FG_STAMPS
     if (l0 == 0 && a.stamps)

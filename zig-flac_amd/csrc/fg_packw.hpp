@@ -63,9 +63,7 @@ __device__ __forceinline__ void stage_dma_w(const uint8_t *pcm, uint64_t off, ui
                 base = ch * 2u * cw;
             }
             if (64u * xi < cst && 64u * xi + l < cst)
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + base + so),
-                                                 (__attribute__((address_space(3))) void *)(stg + ch * cst + 64u * xi), 4,
-                                                 0, 0);
+                lds_dma<4>(src + base + so, stg + ch * cst + 64u * xi);
         }
     }
 }
@@ -153,10 +151,15 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         const uint64_t D = a.offsets[job.slot];
         // split: half 0 ends at bit b0 (header + its subframes); half 1's image starts at byte
         // b0 / 8 and ends with the frame.  Lb = this image's bytes (whole frame: Lt)
+        // every subframe's bits in one load (lane t: subframe t), summed below by readlanes: the
+        // loop over sd0[t].bits was a chain of dependent descriptor reads (r3g stamps: 32 % of a
+        // c4 pack wave's time in the descriptor loads)
+        const uint32_t nsub = NH << ssh;
+        const uint32_t sbits = l < nsub ? sd0[l].bits : 0u;
         uint32_t b0 = 0, base = 0, Lb = Lt;
         if (SPLIT) {
             b0 = 8u * F->hdr_bytes;
-            for (uint32_t t = 0; t < NH; t++) b0 += sd0[t].bits;
+            for (uint32_t t = 0; t < NH; t++) b0 += rdl(sbits, (int)t);
             base = half ? (b0 >> 3) : 0u;
             Lb = half ? Lt - base : (b0 + 7u) >> 3;
         }
@@ -174,7 +177,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         for (int g = 0; g < NG; g++) pq[g] = sd->params[(i0 + 16u * g) >> (12u - o)];
         const uint32_t lb = sd->lane_bits[l0];
         uint32_t sub_start = 8u * F->hdr_bytes;
-        for (uint32_t t = 0; t < sidx; t++) sub_start += sd0[t].bits;
+        for (uint32_t t = 0; t < sidx; t++) sub_start += rdl(sbits, (int)t);
         sub_start -= 8u * base;
 
         // ---- 1. PCM (double-buffered: DMA'd during the previous frame) -> samples
@@ -184,11 +187,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         __syncthreads();
         STAMP(0);
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        // the job record of the frame after next before the DMA: waiting for it then never
+        // waits for the DMA (vmcnt completes in order)
+        FrameJob jnn{};
+        if (nn < n_items) jnn = a.jobs[nn >> ssh];
         if (dbuf && nxt < n_items)
             stage_dma_w(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, dcode, wave, NW, l, drh,
                         nxt & ssh);
-        FrameJob jnn{};
-        if (nn < n_items) jnn = a.jobs[nn >> ssh];
         if (skip) {
             if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
             __syncthreads();
