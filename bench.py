@@ -102,7 +102,9 @@ def parse():
 
 
 def workload_key(a) -> str:
-    return f"{a.config or 'c2'}:{a.frames}x{a.streams}"
+    # the fused single-pass schedule (FLACGPU_FUSED=1) runs other kernels: its own PMC summaries
+    fused = os.environ.get("FLACGPU_FUSED", "0") == "1"
+    return f"{a.config or 'c2'}:{a.frames}x{a.streams}" + ("+fused" if fused else "")
 
 
 def build_input(args, rank):
@@ -676,7 +678,11 @@ def main():
     # longest encode kernel; otherwise the MD5.  Every kernel's own roofline is in `kernels`.
     path_s = sum(per_launch.get(k, 0.0) * lps.get(k, 1) for k in ("analyze", "analyze_tail", "scan", "pack"))
     key = workload_key(args)
-    algo = {"analyze": pcm_bytes, "pack": pcm_bytes + int(fbytes.sum()), "md5": pcm_bytes}
+    # fused single-pass encode (k_analyze<..., FP>, fg_fused.hpp): no pack launch, the analysis
+    # kernel also writes the frames
+    fused = "pack" not in per_launch and "analyze" in per_launch
+    algo = {"analyze": pcm_bytes + (int(fbytes.sum()) if fused else 0), "pack": pcm_bytes + int(fbytes.sum()),
+            "md5": pcm_bytes}
     algo = {k: v // lps.get(k, 1) for k, v in algo.items()}
 
     def kernel_roofline(k):
@@ -760,7 +766,8 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "limiter": LIMITER[dom],
-                "kernel": {"analyze": "k_analyze (4096-sample frames)", "pack": "k_pack4 / k_packw / k_pack",
+                "kernel": {"analyze": "k_analyze<..., FP> (fused analysis + pack, 4096-sample frames)" if fused
+                           else "k_analyze (4096-sample frames)", "pack": "k_pack4 / k_packw / k_pack",
                            "md5": "k_md5_streams_lds"}[dom],
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,

@@ -131,6 +131,13 @@ struct flacgpu_ctx {
     // ovl_ana / ovl_pack workgroups per CU so both are resident on every CU
     uint32_t ovl_chunks = 0, ovl_ana = 2, ovl_pack = 2, ovl_min_frames = 4096;
     bool xcd_queue = true;  // split analysis: per-XCD item queues (fg_device.hpp xcd_ticket)
+    // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp): analysis and pack in
+    // one kernel, frame offsets by an in-kernel look-back over per-slot status words
+    bool fused = false;
+    uint32_t lds_fused = 0, crc_hmaxf = 0;
+    uint16_t *d_crc_powf = nullptr;  // CRC fold shifts for its 256 threads
+    uint64_t *d_status = nullptr;    // per-slot status words, grow-only
+    uint64_t status_cap = 0;
     hipStream_t ovl = nullptr;
     uint64_t *d_cum = nullptr;  // [chunk] bytes of the frames before the chunk's slot range
     HostMd5 host_md5;
@@ -359,6 +366,42 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
         c->scan_part_cap = 0;
         HIPCHK(hipMalloc(&c->d_scan_part, (size_t)nb * 8u));
         c->scan_part_cap = nb;
+    }
+
+    if (c->fused && n_full) {
+        // fused: the tail frames' analysis first (it publishes their sizes), then analysis + pack of
+        // the full frames in one kernel whose frames find their offsets by look-back, then the scan
+        // (offsets of every frame, the total) and the tail frames' pack
+        if (n_frames > c->status_cap) {
+            hipFree(c->d_status);
+            c->d_status = nullptr;
+            c->status_cap = 0;
+            HIPCHK(hipMalloc(&c->d_status, (size_t)n_frames * 8u));
+            c->status_cap = n_frames;
+        }
+        HIPCHK(hipMemsetAsync(c->d_status, 0, (size_t)n_frames * 8u, st));
+        HIPCHK(hipMemsetAsync(c->d_ctr, 0, 4, st));  // the fused kernel's frame queue (ticket 0)
+        a.status = c->d_status;
+        int rc;
+        if (n_tail && (rc = analyze_tail(st))) return rc;
+        {
+            Timed t(c, FLACGPU_K_ANALYZE, st);
+            EncodeArgs h = a;
+            h.jobs = d_jobs;
+            h.n_jobs = (uint32_t)n_full;
+            h.stage_dbuf = 0;
+            h.crc_pow4 = c->d_crc_powf;
+            h.crc_hmax4 = c->crc_hmaxf;
+            h.grid_reserve = c->grid_reserve;
+            HIPCHK(launch_stage(2, h, true, 256u, c->lds_fused, st));
+        }
+        a.status = nullptr;
+        {
+            Timed t(c, FLACGPU_K_SCAN, st);
+            HIPCHK(launch_scan(d_fbytes, d_offsets, d_total, (uint32_t)n_frames, c->d_scan_part, st));
+        }
+        if (n_tail && (rc = pack_tail(st))) return rc;
+        return FLACGPU_OK;
     }
 
     uint32_t K = c->ovl_chunks;
@@ -628,6 +671,12 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
             c->crc_hmaxs = ((img / 4u + 2u * c->nt_psplit - 1u) / (2u * c->nt_psplit)) | 1u;
         }
     }
+    if (c->C == 2 && c->B == 2 && !lpc && c->stereo) {
+        c->fused = false;
+        if (const char *e = std::getenv("FLACGPU_FUSED")) c->fused = e[0] == '1';  // A/B knob
+        c->lds_fused = ana_layout(2, 2, 4, true, false, false, c->image_bytes).total;
+        c->crc_hmaxf = ((c->image_bytes / 4u + 2u * 256u - 1u) / (2u * 256u)) | 1u;
+    }
     if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u ||
         c->lds_pack4 > 160u * 1024u) {
         delete c;
@@ -658,6 +707,14 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     for (uint32_t h = 1; h <= HM4; h++)
         for (uint32_t t = 0; t < T4; t++) pw4[(size_t)(h - 1) * T4 + t] = (uint16_t)q_zpow(16ull + 64ull * h * (T4 - 1u - t));
 
+    if (c->crc_hmaxf) {
+        std::vector<uint16_t> pwf((size_t)c->crc_hmaxf * 256u);
+        for (uint32_t h = 1; h <= c->crc_hmaxf; h++)
+            for (uint32_t t = 0; t < 256u; t++) pwf[(size_t)(h - 1) * 256u + t] = (uint16_t)q_zpow(16ull + 64ull * h * (255u - t));
+        if (hipMalloc(&c->d_crc_powf, pwf.size() * 2) ||
+            hipMemcpy(c->d_crc_powf, pwf.data(), pwf.size() * 2, hipMemcpyHostToDevice))
+            return fail(FLACGPU_ERR_DEVICE);
+    }
     std::vector<uint16_t> pws((size_t)c->crc_hmaxs * c->nt_psplit + 1), x8(24);
     for (uint32_t h = 1; h <= c->crc_hmaxs; h++)
         for (uint32_t t = 0; t < c->nt_psplit; t++)
@@ -697,6 +754,8 @@ void flacgpu_close(flacgpu_ctx *c) {
     for (auto e : c->event_pool) hipEventDestroy(e);
     hipFree(c->d_crc_pow);
     hipFree(c->d_crc_pow4);
+    hipFree(c->d_crc_powf);
+    hipFree(c->d_status);
     hipFree(c->d_crc_join);
     hipFree(c->d_scan_part);
     hipFree(c->d_err);

@@ -139,6 +139,8 @@ struct EncodeArgs {
                                 // stream-MD5 workgroups queued beside this kernel)
     const uint16_t *crc_x8;     // [i] = z^(8 * 2^i) mod P, i < 24 (channel-half pack: CRC shift)
     uint32_t xcd_queue;         // split analysis: items from per-XCD queues (xcd_ticket, fg_device.hpp)
+    uint64_t *status;           // fused encode: per-slot size / inclusive-prefix words (fg_fused.hpp);
+                                // the tail analysis before it publishes its frames' sizes there
     uint32_t grid_per_cu;       // host side: at most this many persistent workgroups per CU (0 = as
                                 // many as fit) -- the overlapped encode shares each CU between an
                                 // analysis grid and a pack grid running on two streams

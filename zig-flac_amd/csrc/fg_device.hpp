@@ -1163,7 +1163,12 @@ __device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int3
 #define FG_PACK_MINW 4
 #endif
 
-template <int B, int CLS, bool FULL, int MAXT, int NC, int LPW>
+#include "fg_fused.hpp"
+
+template <int B, int CLS, bool FULL, int MAXT, int NC, int LPW, bool FP = false>
+// FP  : fused single-pass encode (full 16-bit stereo frames only, fg_fused.hpp): the workgroup
+//       packs the frame it analysed; frames come from the ticket queue one at a time (no
+//       prefetch) and the staging is single-buffered (it becomes the frame image)
 // i64 samples (32-bit input), the tail kernels' LDS tables and the LPC search need
 // the larger register budget (2 waves/SIMD); the rest fits 128 VGPRs (4 waves/SIMD).
 //   LPW  : 0 = fixed prediction only (the reference); 8 / 12 = LPC taps held in
@@ -1186,7 +1191,8 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     const uint32_t cw = 16u * C * B;           // dwords per 64-sample chunk
     const uint32_t cst = cw + stage_pad(C, B);  // LDS chunk stride (dwords)
     const bool dbuf = FULL && a.stage_dbuf != 0;
-    const AnaLayout LY = ana_layout(C, B, NW, FULL, dbuf, LPW > 0);
+    static_assert(!FP || (B == 2 && CLS == 16 && FULL && MAXT == 256 && NC == 2 && LPW == 0), "fused: C2 only");
+    const AnaLayout LY = ana_layout(C, B, NW, FULL, dbuf, LPW > 0, FP ? a.image_bytes : 0u);
     uint8_t *par = smem + LY.par + wave * LY.par_stride;
     uint32_t *recs = (uint32_t *)(smem + LY.rec);
     uint32_t *misc = (uint32_t *)(smem + LY.misc);
@@ -1217,7 +1223,11 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     const uint32_t drh = ssh ? C * (uint32_t)B / 4u : 0u;
     const uint32_t n_items = a.n_jobs << ssh;
     if (tid == 0) {
-        if (xq) {
+        if (FP) {
+            // fused: every frame from the queue, taken when its processing starts (a workgroup
+            // never holds a frame it has not started: the look-back waits only on running ones)
+            misc[22] = atomicAdd(ctr, 1u);
+        } else if (xq) {
             misc[22] = xcd_ticket(xqc, a.n_jobs);
             misc[21] = xcd_ticket(xqc, a.n_jobs);
         } else {
@@ -1237,7 +1247,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     // estimate barrier (step 9).  Taken after the DMA of the next frame's PCM, the wait for the
     // atomic's value also waited for that DMA.
     uint32_t tk = 0;
-    if (tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
+    if (!FP && tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
     while (jidx < n_items) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
         const uint32_t half = jidx & ssh;
@@ -1862,12 +1872,15 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             uint32_t *rc = recs + cand * 16u;
             rc[6] = (uint32_t)R.est; rc[7] = (uint32_t)(R.est >> 32);
         }
-        if (tid == 0) misc[20] = tk;
+        if (!FP && tid == 0) misc[20] = tk;
         bar_lds();
         // the job record of the frame after next (DMA'd at the top of the next frame)
-        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        uint32_t nn = 0;
         FrameJob jnn{};
-        if (nn < n_items) jnn = a.jobs[nn >> ssh];
+        if constexpr (!FP) {
+            nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+            if (nn < n_items) jnn = a.jobs[nn >> ssh];
+        }
         uint32_t channel_code, n_out;
         int my_slot;
         if (stereo) {
@@ -2009,10 +2022,21 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         if (l == 0 && my_slot >= 0) misc[40 + my_slot] = sub_bits;
         STAMP(7);
 
-        // ---- 11. the frame descriptor
+        // ---- 11. the frame descriptor (fused: the written subframes' fields in LDS, see below)
         uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
         const uint8_t *pp = par + cur * 512u + ((1u << R.porder) - 1u);
-        if (my_slot >= 0) {
+        if (FP && my_slot >= 0) {
+            uint32_t *lbits = (uint32_t *)(smem + LY.lbits);
+            lbits[64u * (uint32_t)my_slot + l] = seg;
+            if (l == 0) {
+                misc[44 + my_slot] = cand;
+                misc[46 + my_slot] = R.type | (R.waste << 8) | (R.bd << 16) | (R.order << 24);
+                misc[48 + my_slot] = R.porder | (R.method << 8);
+                misc[50 + 2 * my_slot] = (uint32_t)R.cval;
+                misc[51 + 2 * my_slot] = (uint32_t)((uint64_t)R.cval >> 32);
+            }
+        }
+        if (!FP && my_slot >= 0) {
             SubDesc *sd = (SubDesc *)(fd + sizeof(FrameDesc)) + my_slot;  // (split: the global channel)
             if (l == 0) {
                 sd->type = (uint8_t)R.type;
@@ -2036,8 +2060,18 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 for (uint32_t j = l; j < np; j += 64) sd->params[j] = pp[j];
             }
         }
-        __syncthreads();  // every written wave's sub_bits
-        if (tid == 0 && half == 0) {
+        if (FP) bar_lds();  // every written wave's sub_bits and fields (LDS only)
+        else __syncthreads();  // every written wave's sub_bits
+        if (FP && tid == 0) {
+            uint32_t total = 8u * misc[18];
+            for (uint32_t c = 0; c < n_out; c++) total += misc[40 + c];
+            misc[17] = total;
+            const uint32_t fbytes = ((total + 7u) >> 3) + 2u;
+            if (fbytes + 16u > a.image_bytes) atomicOr(a.err, 1u);  // the image bound
+            a.frame_bytes[job.slot] = fbytes;
+            st_publish(a.status, job.slot, kStAgg | fbytes);  // before any wait (fg_fused.hpp)
+        }
+        if (!FP && tid == 0 && half == 0) {
             const uint32_t *hw = misc + 32;
             const uint32_t hb = misc[18];
             FrameDesc *f = (FrameDesc *)fd;
@@ -2052,6 +2086,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 const uint32_t fbytes = ((total + 7u) >> 3) + 2u;
                 if (fbytes + 16u > a.image_bytes) atomicOr(a.err, 1u);  // the pack kernel's image bound
                 a.frame_bytes[job.slot] = fbytes;
+                if (a.status) st_publish(a.status, job.slot, kStAgg | fbytes);  // fused launch follows
                 misc[17] = fbytes;
             }
         }
@@ -2087,7 +2122,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             if (tid == 0 && half == 0) {
                 fr->channel_code = channel_code;
                 fr->n_cand = NW << ssh;
-                if (!ssh) fr->frame_bytes = misc[17];  // (split: k_frame_totals)
+                if (!ssh) fr->frame_bytes = FP ? ((misc[17] + 7u) >> 3) + 2u : misc[17];  // (split: k_frame_totals)
                 fr->pad = 0;
             }
         }
@@ -2095,6 +2130,18 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // nothing touches LDS between here and the next frame's top barrier, which then orders
         // this frame's last reads before the next frame's writes; synchronous staging writes the
         // staging buffer before that barrier, so it needs its own
+        if constexpr (FP) {
+            // ---- 13. fused: pack the frame from the staged PCM (fg_fused.hpp), then the next ticket
+            bar_lds();  // records read misc[17]
+            fused_pack(a, stg, misc, (const uint32_t *)(smem + LY.lbits), smem + LY.par, LY.par_stride, job.slot,
+                       misc[17], tid, wave, l);
+            if (tid == 0) misc[22] = atomicAdd(ctr, 1u);
+            __syncthreads();  // the image is read by the stores; the next frame's DMA overwrites it
+            jidx = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[22]);
+            if (jidx < n_items) job = a.jobs[jidx];
+            STAMP(6);
+            continue;
+        }
         if (!dbuf) __syncthreads();
         if (tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
         STAMP(6);
@@ -2523,7 +2570,11 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
         // full 16-bit two-channel frames: four waves per written subframe (fg_pack4.hpp)
         if (stage == 1 && full && a.channels == 2 && threads == 512u)
             return launch_persistent(k_pack4<512>, a, threads, lds, st);
+        // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp)
+        if (stage == 2 && full && a.channels == 2 && a.stereo && threads == 256u)
+            return launch_persistent(k_analyze<2, 16, true, 256, 2, 0, true>, a, threads, lds, st);
     }
+    if (stage == 2) return hipErrorInvalidValue;
     // other full frames: WPS waves per written subframe (fg_packw.hpp); the host marks it by
     // the thread count 64 * n_out * WPS (k_pack runs 64 * n_out)
     if (stage == 1 && full && a.ch_split) {

@@ -18,6 +18,7 @@ struct AnaLayout {
     uint32_t lpc;    // LPC: quantised coefficient table, kLpcTab i32 per wave
     uint32_t rec;    // 16 x u32 per candidate wave
     uint32_t misc;   // 64 x u32 scratch (header words)
+    uint32_t lbits;  // fused encode: 2 x 64 u32 segment bits of the written subframes (== total without)
     uint32_t total;
 };
 
@@ -53,10 +54,13 @@ __host__ __device__ inline uint32_t stage_bytes(uint32_t C, uint32_t B) {
 // The full-frame kernel double-buffers it when both buffers fit and DMAs the
 // next frame's PCM into the idle one; the tail kernel (and configs whose two
 // buffers do not fit) stage synchronously into one buffer.
+// fused_img != 0 (the fused encode, fg_fused.hpp): the single staging buffer also holds the frame
+// image of that many bytes, and lbits follows misc
 __host__ __device__ inline AnaLayout ana_layout(uint32_t C, uint32_t B, uint32_t nw, bool full, bool dbuf,
-                                                bool lpc = false) {
+                                                bool lpc = false, uint32_t fused_img = 0) {
     AnaLayout L;
-    const uint32_t sb = fg_round16(stage_bytes(C, B));
+    uint32_t sb = fg_round16(stage_bytes(C, B));
+    if (fused_img > sb) sb = fg_round16(fused_img);
     uint32_t end = sb;
     L.stage0 = L.stage1 = 0;
     if (full && dbuf) {
@@ -73,7 +77,8 @@ __host__ __device__ inline AnaLayout ana_layout(uint32_t C, uint32_t B, uint32_t
     L.lpc = L.par + nw * L.par_stride;
     L.rec = L.lpc + (lpc ? nw * 4u * (uint32_t)kLpcTab : 0u);
     L.misc = L.rec + nw * 64u;
-    L.total = fg_round16(L.misc + 256u);
+    L.lbits = L.misc + 256u;
+    L.total = fg_round16(L.lbits + (fused_img ? 512u : 0u));
     return L;
 }
 

@@ -69,7 +69,6 @@ __device__ __forceinline__ void p4_dsc_dma(const EncodeArgs &a, uint32_t slot, u
 
 template <int MAXT>
 __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
-    constexpr uint32_t C = 2, B = 2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
     const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
