@@ -86,7 +86,7 @@ def parse():
     p.add_argument("--no-curve", action="store_true")
     p.add_argument("--curve", default="8,64,1024,8192,16384,32768,65536")
     p.add_argument("--no-e2e", action="store_true")
-    p.add_argument("--e2e-files", default="8,16,32", help="file counts of the end-to-end curve")
+    p.add_argument("--e2e-files", default="8,16,32,64", help="file counts of the end-to-end curve")
     p.add_argument("--e2e-minutes", type=float, default=10.0)
     p.add_argument("--no-sharded", action="store_true", help="skip the sharded single-stream line")
     p.add_argument("--sharded-config", choices=sorted(PRESETS), default="c4")
@@ -491,8 +491,11 @@ def end_to_end(args):
                 "host_md5_cores_x_rate": round(share * md5_gbs * 1e3 / fb, 1), "cores": share,
                 "one_file_md5_floor_ms": round(md5_s * 1e3, 2)},
             "path": "pinned host PCM -> flacgpu_encode_file per file (one context + host thread each): H2D, "
-                    "kernels, D2H pipelined in 2048-frame chunks; MD5 on a host thread per file beside the "
-                    "encode; 73-byte header + frames in host memory (pinned)",
+                    "kernels, D2H pipelined in 2048-frame chunks; each file's MD5 on the library's host hashing "
+                    "pool beside the encode (up to 4 files' chains interleaved per core, fg_md5_host.cpp; "
+                    "FLACGPU_MD5_THREADS=-1: one plain chain per file); 73-byte header + frames in host memory "
+                    "(pinned)",
+            "md5_pool_threads": os.environ.get("FLACGPU_MD5_THREADS", "default (CPUs of the affinity mask)"),
             "output_ok": bool(ok)}
 
 

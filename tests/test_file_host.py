@@ -207,3 +207,17 @@ def test_cpp_encoder_api_matches_oracle_file(tmp_path, ch, bits, rate, n):
     out = tmp_path / "o.flac"
     subprocess.check_call([exe, str(raw), str(ch), str(bits), str(rate), str(out)])
     assert out.read_bytes() == oracle_ref.encode_file(pcm, ch, bits, rate)
+
+
+@pytest.mark.parametrize("threads", ["1", "3"])
+def test_host_md5_pool_matches_plain_chain(threads):
+    """fg_md5_host.cpp's hashing pool (the file path's MD5 engine: up to four callers' chains
+    interleaved per worker) equals one plain chain per message, many callers at once, updates split
+    at odd offsets (tests/cpp/md5_pool_test.cpp)."""
+    import os
+    import subprocess
+
+    subprocess.check_call(["make", "-s", "-C", CPP_DIR, "build/md5_pool_test"])
+    r = subprocess.run([os.path.join(CPP_DIR, "build", "md5_pool_test")], capture_output=True, text=True,
+                       env=dict(os.environ, FLACGPU_MD5_THREADS=threads), timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr

@@ -175,7 +175,8 @@ int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sa
     const bool host_md5 = flacgpu_md5_get_engine(ctx) == FLACGPU_MD5_HOST;
     if (host_md5) {
         try {
-            hasher = std::thread([&]() { md5.update(pcm, pcm_bytes); });
+            // the process-wide pool interleaves this file's chain with other files hashed at once
+            hasher = std::thread([&]() { fg::md5_pool_update(&md5, pcm, pcm_bytes); });
         } catch (const std::system_error &) {
             md5.update(pcm, pcm_bytes);  // no thread to be had: hash here, before the encode
         }

@@ -1,7 +1,16 @@
 // fg_md5_host.cpp -- host MD5 (see fg_md5_host.hpp).
 #include "fg_md5_host.hpp"
 
+#include <sched.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 namespace fg {
 namespace {
@@ -63,7 +72,197 @@ void compress(uint32_t st[4], const uint8_t *blk, size_t nblocks) {
     st[3] = d0;
 }
 
+// N independent messages, nblocks blocks each, one step of every chain after the other: the
+// chains are independent, so an out-of-order core overlaps them (one MD5 chain is latency-bound
+// on ~4 dependent ALU ops per step and leaves most execution ports idle).
+template <int N>
+void compress_n(uint32_t *const st[N], const uint8_t *const blk0[N], size_t nblocks) {
+    uint32_t a0[N], b0[N], c0[N], d0[N];
+    const uint8_t *blk[N];
+    for (int j = 0; j < N; j++) {
+        a0[j] = st[j][0]; b0[j] = st[j][1]; c0[j] = st[j][2]; d0[j] = st[j][3];
+        blk[j] = blk0[j];
+    }
+    for (size_t n = 0; n < nblocks; n++) {
+        uint32_t X[N][16], a[N], b[N], c[N], d[N];
+        for (int j = 0; j < N; j++) {
+            memcpy(X[j], blk[j], 64);
+            blk[j] += 64;
+            a[j] = a0[j]; b[j] = b0[j]; c[j] = c0[j]; d[j] = d0[j];
+        }
+#define H5N(F, A, B, C, D, i, k, s) \
+    for (int j = 0; j < N; j++) H5STEP(F, A[j], B[j], C[j], D[j], X[j][i], k, s);
+        H5N(H5F, a, b, c, d, 0, 0xd76aa478, 7)   H5N(H5F, d, a, b, c, 1, 0xe8c7b756, 12)
+        H5N(H5F, c, d, a, b, 2, 0x242070db, 17)  H5N(H5F, b, c, d, a, 3, 0xc1bdceee, 22)
+        H5N(H5F, a, b, c, d, 4, 0xf57c0faf, 7)   H5N(H5F, d, a, b, c, 5, 0x4787c62a, 12)
+        H5N(H5F, c, d, a, b, 6, 0xa8304613, 17)  H5N(H5F, b, c, d, a, 7, 0xfd469501, 22)
+        H5N(H5F, a, b, c, d, 8, 0x698098d8, 7)   H5N(H5F, d, a, b, c, 9, 0x8b44f7af, 12)
+        H5N(H5F, c, d, a, b, 10, 0xffff5bb1, 17) H5N(H5F, b, c, d, a, 11, 0x895cd7be, 22)
+        H5N(H5F, a, b, c, d, 12, 0x6b901122, 7)  H5N(H5F, d, a, b, c, 13, 0xfd987193, 12)
+        H5N(H5F, c, d, a, b, 14, 0xa679438e, 17) H5N(H5F, b, c, d, a, 15, 0x49b40821, 22)
+        H5N(H5G, a, b, c, d, 1, 0xf61e2562, 5)   H5N(H5G, d, a, b, c, 6, 0xc040b340, 9)
+        H5N(H5G, c, d, a, b, 11, 0x265e5a51, 14) H5N(H5G, b, c, d, a, 0, 0xe9b6c7aa, 20)
+        H5N(H5G, a, b, c, d, 5, 0xd62f105d, 5)   H5N(H5G, d, a, b, c, 10, 0x02441453, 9)
+        H5N(H5G, c, d, a, b, 15, 0xd8a1e681, 14) H5N(H5G, b, c, d, a, 4, 0xe7d3fbc8, 20)
+        H5N(H5G, a, b, c, d, 9, 0x21e1cde6, 5)   H5N(H5G, d, a, b, c, 14, 0xc33707d6, 9)
+        H5N(H5G, c, d, a, b, 3, 0xf4d50d87, 14)  H5N(H5G, b, c, d, a, 8, 0x455a14ed, 20)
+        H5N(H5G, a, b, c, d, 13, 0xa9e3e905, 5)  H5N(H5G, d, a, b, c, 2, 0xfcefa3f8, 9)
+        H5N(H5G, c, d, a, b, 7, 0x676f02d9, 14)  H5N(H5G, b, c, d, a, 12, 0x8d2a4c8a, 20)
+        H5N(H5H, a, b, c, d, 5, 0xfffa3942, 4)   H5N(H5H, d, a, b, c, 8, 0x8771f681, 11)
+        H5N(H5H, c, d, a, b, 11, 0x6d9d6122, 16) H5N(H5H, b, c, d, a, 14, 0xfde5380c, 23)
+        H5N(H5H, a, b, c, d, 1, 0xa4beea44, 4)   H5N(H5H, d, a, b, c, 4, 0x4bdecfa9, 11)
+        H5N(H5H, c, d, a, b, 7, 0xf6bb4b60, 16)  H5N(H5H, b, c, d, a, 10, 0xbebfbc70, 23)
+        H5N(H5H, a, b, c, d, 13, 0x289b7ec6, 4)  H5N(H5H, d, a, b, c, 0, 0xeaa127fa, 11)
+        H5N(H5H, c, d, a, b, 3, 0xd4ef3085, 16)  H5N(H5H, b, c, d, a, 6, 0x04881d05, 23)
+        H5N(H5H, a, b, c, d, 9, 0xd9d4d039, 4)   H5N(H5H, d, a, b, c, 12, 0xe6db99e5, 11)
+        H5N(H5H, c, d, a, b, 15, 0x1fa27cf8, 16) H5N(H5H, b, c, d, a, 2, 0xc4ac5665, 23)
+        H5N(H5I, a, b, c, d, 0, 0xf4292244, 6)   H5N(H5I, d, a, b, c, 7, 0x432aff97, 10)
+        H5N(H5I, c, d, a, b, 14, 0xab9423a7, 15) H5N(H5I, b, c, d, a, 5, 0xfc93a039, 21)
+        H5N(H5I, a, b, c, d, 12, 0x655b59c3, 6)  H5N(H5I, d, a, b, c, 3, 0x8f0ccc92, 10)
+        H5N(H5I, c, d, a, b, 10, 0xffeff47d, 15) H5N(H5I, b, c, d, a, 1, 0x85845dd1, 21)
+        H5N(H5I, a, b, c, d, 8, 0x6fa87e4f, 6)   H5N(H5I, d, a, b, c, 15, 0xfe2ce6e0, 10)
+        H5N(H5I, c, d, a, b, 6, 0xa3014314, 15)  H5N(H5I, b, c, d, a, 13, 0x4e0811a1, 21)
+        H5N(H5I, a, b, c, d, 4, 0xf7537e82, 6)   H5N(H5I, d, a, b, c, 11, 0xbd3af235, 10)
+        H5N(H5I, c, d, a, b, 2, 0x2ad7d2bb, 15)  H5N(H5I, b, c, d, a, 9, 0xeb86d391, 21)
+#undef H5N
+        for (int j = 0; j < N; j++) {
+            a0[j] += a[j]; b0[j] += b[j]; c0[j] += c[j]; d0[j] += d[j];
+        }
+    }
+    for (int j = 0; j < N; j++) {
+        st[j][0] = a0[j]; st[j][1] = b0[j]; st[j][2] = c0[j]; st[j][3] = d0[j];
+    }
+}
+
+// The process-wide hashing pool (Md5Pool below): a job is one whole-buffer update of a HostMd5.
+struct Md5Job {
+    HostMd5 *h;
+    const uint8_t *p;  // the job's next full block
+    size_t nb;         // full blocks left
+    const uint8_t *tail;
+    size_t tail_len;
+    bool done = false;
+};
+
+class Md5Pool {
+  public:
+    static Md5Pool &get() {
+        // never destroyed: its detached workers wait on its condition variable until the process
+        // ends (a static object's destructor would destroy it under them at exit)
+        static Md5Pool *pool = new Md5Pool;
+        return *pool;
+    }
+    // hash `len` bytes into h on a pool worker, interleaved with other callers' jobs; blocks
+    void run(HostMd5 *h, const uint8_t *p, size_t len) {
+        // the partial block in h first (on the caller: at most 63 bytes of copying)
+        if (h->fill && len) {
+            const size_t take = len < 64u - h->fill ? len : 64u - h->fill;
+            h->update(p, take);
+            p += take;
+            len -= take;
+        }
+        if (h->fill || len < 64u * 64u || workers_ == 0) {  // short updates: no hand-off
+            h->update(p, len);
+            return;
+        }
+        Md5Job job;
+        job.h = h;
+        job.p = p;
+        job.nb = len / 64u;
+        job.tail = p + job.nb * 64u;
+        job.tail_len = len - job.nb * 64u;
+        h->bytes += job.nb * 64u;
+        {
+            std::unique_lock<std::mutex> lk(m_);
+            q_.push_back(&job);
+            cv_.notify_one();
+            done_cv_.wait(lk, [&] { return job.done; });
+        }
+        h->update(job.tail, job.tail_len);
+    }
+
+  private:
+    static constexpr int kMaxChains = 4;
+    static constexpr size_t kChunk = 256;  // blocks per chain between queue checks
+    Md5Pool() {
+        int n = 0;
+        if (const char *e = std::getenv("FLACGPU_MD5_THREADS")) n = std::atoi(e);  // < 0: no pool (A/B)
+        if (n == 0) {
+            // the CPU share: OMP_NUM_THREADS where the environment states it (a cgroup quota is
+            // not visible in the affinity mask), else the affinity mask; the callers mostly wait
+            // on the GPU
+            if (const char *e = std::getenv("OMP_NUM_THREADS")) n = std::atoi(e);
+            if (n <= 0) {
+                cpu_set_t set;
+                n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+            }
+        }
+        if (n > 64) n = 64;
+        if (n < 0) n = 0;  // every caller hashes its own chain
+        for (int i = 0; i < n; i++) {
+            try {
+                std::thread([this] { loop(); }).detach();
+                workers_++;
+            } catch (...) {
+                break;
+            }
+        }
+    }
+    void loop() {
+        std::vector<Md5Job *> act;
+        for (;;) {
+            {
+                // an idle worker takes one message; a busy one adds more only while no worker is
+                // idle (so a few files spread over the workers, many files share them)
+                std::unique_lock<std::mutex> lk(m_);
+                if (act.empty()) {
+                    idle_++;
+                    cv_.wait(lk, [&] { return !q_.empty(); });
+                    idle_--;
+                }
+                while ((int)act.size() < kMaxChains && !q_.empty() && (act.empty() || idle_ == 0)) {
+                    act.push_back(q_.front());
+                    q_.pop_front();
+                }
+            }
+            size_t nb = kChunk;
+            for (auto *j : act) nb = j->nb < nb ? j->nb : nb;
+            uint32_t *st[kMaxChains];
+            const uint8_t *bp[kMaxChains];
+            for (size_t i = 0; i < act.size(); i++) {
+                st[i] = act[i]->h->h;
+                bp[i] = act[i]->p;
+            }
+            switch (act.size()) {
+            case 1: compress_n<1>(st, bp, nb); break;
+            case 2: compress_n<2>(st, bp, nb); break;
+            case 3: compress_n<3>(st, bp, nb); break;
+            default: compress_n<4>(st, bp, nb); break;
+            }
+            bool finished = false;
+            for (auto *j : act) {
+                j->p += nb * 64u;
+                j->nb -= nb;
+                finished |= j->nb == 0;
+            }
+            if (finished) {
+                std::lock_guard<std::mutex> lk(m_);
+                for (auto *j : act)
+                    if (j->nb == 0) j->done = true;
+                done_cv_.notify_all();
+                act.erase(std::remove_if(act.begin(), act.end(), [](Md5Job *j) { return j->done; }), act.end());
+            }
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<Md5Job *> q_;
+    int workers_ = 0, idle_ = 0;
+};
+
 }  // namespace
+
+void md5_pool_update(HostMd5 *h, const void *data, size_t len) { Md5Pool::get().run(h, (const uint8_t *)data, len); }
 
 void HostMd5::reset() {
     h[0] = 0x67452301u;

@@ -20,4 +20,12 @@ struct HostMd5 {
     void final(uint8_t digest[16]);  // pads, writes the digest, resets
 };
 
+// h->update(data, len) on the process-wide hashing pool (fg_md5_host.cpp): the bulk of a long
+// update runs on a pool worker that hashes up to four callers' messages at once, their chains
+// interleaved step by step (one MD5 chain leaves most of a core's ALU ports idle), so files
+// encoded concurrently hash 2-3x faster per core than one scalar chain each.  Blocks until done.
+// FLACGPU_MD5_THREADS sets the worker count (default: OMP_NUM_THREADS, else the affinity mask's
+// CPUs; -1: no pool, each caller hashes its own chain).
+void md5_pool_update(HostMd5 *h, const void *data, size_t len);
+
 }  // namespace fg
