@@ -614,8 +614,9 @@ def cpu_baseline(buf, args):
         "cpu_model": facts["model"],
         "cores_per_socket": cps,
         "sockets": facts["sockets"],
-        "build": "oracle/flac_oracle.c -O3 -march=x86-64-v4 (scalar C restatement; the Zig reference is "
-                 "unbuildable here: no Zig 0.16 on the box)",
+        "build": "oracle/flac_oracle.c -O3 -march=x86-64-v4 (C restatement, CRC-16 by slicing-by-8 tables "
+                 "since r3w where the reference folds with PCLMUL; the Zig reference is unbuildable here: no "
+                 "Zig 0.16 on the box)",
         "per_core": round(value / P, 3),
         "single_socket_estimate": round(value / P * cps, 1) if cps else None,
         "single_socket_note": f"measured at P = {P} threads (the box's CPU share for one GPU) of {cps} cores per "

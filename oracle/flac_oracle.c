@@ -30,13 +30,43 @@ uint8_t oracle_crc8(const uint8_t *p, size_t n) {
 }
 
 /* CRC-16/UMTS (crc16.zig:15-57; the PCLMUL fold and the std table fallback
- * are the same function): poly 0x8005, init 0, MSB first (check 0xFEE8).   */
-uint16_t oracle_crc16(uint16_t crc, const uint8_t *p, size_t n) {
+ * are the same function): poly 0x8005, init 0, MSB first (check 0xFEE8).
+ * oracle_crc16_bitwise is the definition, one bit per step; oracle_crc16 computes the same
+ * value eight bytes per step from eight 256-entry tables (slicing-by-8), so the CPU-baseline
+ * build does not time a bit-serial loop where the reference folds with PCLMUL
+ * (tests/test_oracle_kat.py checks the two against each other).                         */
+uint16_t oracle_crc16_bitwise(uint16_t crc, const uint8_t *p, size_t n) {
     for (size_t i = 0; i < n; i++) {
         crc ^= (uint16_t)(p[i] << 8);
         for (int b = 0; b < 8; b++)
             crc = (uint16_t)((crc & 0x8000) ? (crc << 1) ^ 0x8005 : (crc << 1));
     }
+    return crc;
+}
+
+/* T[k][v]: the register contribution of byte value v followed by k zero bytes */
+static uint16_t crc16_tab[8][256];
+__attribute__((constructor)) static void crc16_tab_init(void) {
+    for (int v = 0; v < 256; v++) {
+        uint8_t b = (uint8_t)v;
+        crc16_tab[0][v] = oracle_crc16_bitwise(0, &b, 1);
+    }
+    for (int k = 1; k < 8; k++)
+        for (int v = 0; v < 256; v++) {
+            const uint16_t t = crc16_tab[k - 1][v];
+            crc16_tab[k][v] = (uint16_t)((t << 8) ^ crc16_tab[0][t >> 8]);
+        }
+}
+
+uint16_t oracle_crc16(uint16_t crc, const uint8_t *p, size_t n) {
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const uint8_t b0 = (uint8_t)(p[i] ^ (crc >> 8)), b1 = (uint8_t)(p[i + 1] ^ (crc & 0xff));
+        crc = (uint16_t)(crc16_tab[7][b0] ^ crc16_tab[6][b1] ^ crc16_tab[5][p[i + 2]] ^ crc16_tab[4][p[i + 3]] ^
+                         crc16_tab[3][p[i + 4]] ^ crc16_tab[2][p[i + 5]] ^ crc16_tab[1][p[i + 6]] ^
+                         crc16_tab[0][p[i + 7]]);
+    }
+    for (; i < n; i++) crc = (uint16_t)((crc << 8) ^ crc16_tab[0][(crc >> 8) ^ p[i]]);
     return crc;
 }
 

@@ -82,6 +82,7 @@ typedef struct {
 /* ---- primitives ---- */
 uint8_t oracle_crc8(const uint8_t *p, size_t n);               /* CRC-8/SMBUS */
 uint16_t oracle_crc16(uint16_t crc, const uint8_t *p, size_t n); /* CRC-16/UMTS */
+uint16_t oracle_crc16_bitwise(uint16_t crc, const uint8_t *p, size_t n); /* the same, one bit per step */
 
 typedef struct {
     uint32_t a, b, c, d;

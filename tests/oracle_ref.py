@@ -56,6 +56,7 @@ def lib(fast: bool = False):
         L = ctypes.CDLL(LIB)
         L.oracle_crc8.restype = ctypes.c_uint8
         L.oracle_crc16.restype = ctypes.c_uint16
+        L.oracle_crc16_bitwise.restype = ctypes.c_uint16
         L.oracle_encode_frame.restype = ctypes.c_long
         L.oracle_encode_stream.restype = ctypes.c_long
         L.oracle_encode_file.restype = ctypes.c_long

@@ -32,6 +32,20 @@ def test_crc16_incremental():
     assert c == L.oracle_crc16(0, data, len(data))
 
 
+
+def test_crc16_sliced_equals_bitwise():
+    """oracle_crc16 (slicing-by-8 tables) equals the one-bit-per-step definition for every
+    start value class, length 0..70 (both the 8-byte body and the byte tail) and random data."""
+    import random
+
+    L = oracle_ref.lib()
+    assert L.oracle_crc16_bitwise(0, b"123456789", 9) == 0xFEE8
+    rnd = random.Random(7)
+    for n in list(range(71)) + [4096, 10357]:
+        data = bytes(rnd.randrange(256) for _ in range(n))
+        for crc in (0, 0xFFFF, rnd.randrange(65536)):
+            assert L.oracle_crc16(crc, data, n) == L.oracle_crc16_bitwise(crc, data, n), (n, crc)
+
 RFC1321 = [
     (b"", "d41d8cd98f00b204e9800998ecf8427e"),
     (b"a", "0cc175b9c0f1b6a831c399e269772661"),
