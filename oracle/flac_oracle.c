@@ -89,27 +89,35 @@ static const uint8_t MD5_S[64] = {7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7
 
 static uint32_t rol32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
 
+/* RFC 1321 section 3.4: 64 steps in four rounds of 16, each round's loop fully unrolled so
+ * the step's constant, shift and message word index are immediates (the branch-per-step form
+ * hashed at 311 MB/s against OpenSSL's 498 on the same core; the CPU baseline times this). */
+#define MD5_ROUND(FN, G)                                                   \
+    _Pragma("GCC unroll 16") for (int j = 0; j < 16; j++) {                \
+        const int i = r0 + j;                                              \
+        const uint32_t f = FN, t = d;                                      \
+        d = cc;                                                            \
+        cc = b;                                                            \
+        b = b + rol32(a + f + MD5_K[i] + m[(G) & 15], MD5_S[i]);            \
+        a = t;                                                             \
+    }
 static void md5_block(oracle_md5_ctx *c, const uint8_t *blk) {
     uint32_t m[16];
     for (int i = 0; i < 16; i++)
         m[i] = (uint32_t)blk[4 * i] | ((uint32_t)blk[4 * i + 1] << 8) | ((uint32_t)blk[4 * i + 2] << 16) |
                ((uint32_t)blk[4 * i + 3] << 24);
     uint32_t a = c->a, b = c->b, cc = c->c, d = c->d;
-    for (int i = 0; i < 64; i++) {
-        uint32_t f;
-        int g;
-        if (i < 16) { f = (b & cc) | (~b & d); g = i; }
-        else if (i < 32) { f = (d & b) | (~d & cc); g = (5 * i + 1) & 15; }
-        else if (i < 48) { f = b ^ cc ^ d; g = (3 * i + 5) & 15; }
-        else { f = cc ^ (b | ~d); g = (7 * i) & 15; }
-        uint32_t t = d;
-        d = cc;
-        cc = b;
-        b = b + rol32(a + f + MD5_K[i] + m[g], MD5_S[i]);
-        a = t;
-    }
+    int r0 = 0;
+    MD5_ROUND((b & cc) | (~b & d), i)
+    r0 = 16;
+    MD5_ROUND((d & b) | (~d & cc), 5 * i + 1)
+    r0 = 32;
+    MD5_ROUND(b ^ cc ^ d, 3 * i + 5)
+    r0 = 48;
+    MD5_ROUND(cc ^ (b | ~d), 7 * i)
     c->a += a; c->b += b; c->c += cc; c->d += d;
 }
+#undef MD5_ROUND
 
 void oracle_md5_init(oracle_md5_ctx *c) {
     c->a = 0x67452301; c->b = 0xefcdab89; c->c = 0x98badcfe; c->d = 0x10325476;
