@@ -409,21 +409,39 @@ int oracle_best_order(const int64_t *s, uint32_t n, int wide, uint64_t totals[5]
 
 /* calcResiduals (fixed.zig:30-76,169-201): COEFF_SCALAR stencil, wrapping
  * i32 (narrow) or i64 truncated to the low 32 bits (wide).  e[0..k) unused. */
-static const int32_t COEFF[5][4] = {{0, 0, 0, 0}, {1, 0, 0, 0}, {-1, 2, 0, 0}, {1, -3, 3, 0}, {-1, 4, -6, 4}};
+/* COEFF_SCALAR = {}, {1}, {-1, 2}, {1, -3, 3}, {-1, 4, -6, 4}: the residual is x_i minus them
+ * applied to x_{i-k} .. x_{i-1}, expanded below per order */
 static void calc_residuals(const int64_t *s, uint32_t n, unsigned k, int wide, int32_t *e) {
-    for (uint32_t i = 0; i < n; i++) {
-        if (i < k) { e[i] = 0; continue; }
-        if (k == 0) { e[i] = (int32_t)(uint32_t)(uint64_t)s[i]; continue; }
-        if (wide) {
-            uint64_t pred = 0;
-            for (unsigned j = 0; j < k; j++) pred += (uint64_t)(int64_t)COEFF[k][j] * (uint64_t)s[i - k + j];
-            e[i] = (int32_t)(uint32_t)((uint64_t)s[i] - pred);
-        } else {
-            uint32_t pred = 0;
-            for (unsigned j = 0; j < k; j++) pred += (uint32_t)COEFF[k][j] * (uint32_t)(int32_t)s[i - k + j];
-            e[i] = (int32_t)((uint32_t)(int32_t)s[i] - pred);
+    /* one branch-free loop per (order, width) with the stencil as immediates, so the compiler
+     * vectorises it as the reference does (calcResidualVec, fixed.zig:169-201) */
+    uint32_t i = 0;
+    for (; i < k && i < n; i++) e[i] = 0;
+    /* X(j) = sample i - j in the loop's width (i >= k here, so every X(j), j <= k, is in range) */
+#define X(j) ((T)s[i - (j)])
+#define RES_LOOP(T_, EXPR)                                                  \
+    {                                                                       \
+        typedef T_ T;                                                       \
+        for (; i < n; i++) e[i] = (int32_t)(uint32_t)(EXPR);                \
+    }
+    if (wide) {
+        switch (k) {
+        case 0: RES_LOOP(uint64_t, X(0)) break;
+        case 1: RES_LOOP(uint64_t, X(0) - X(1)) break;
+        case 2: RES_LOOP(uint64_t, X(0) - 2 * X(1) + X(2)) break;
+        case 3: RES_LOOP(uint64_t, X(0) - 3 * X(1) + 3 * X(2) - X(3)) break;
+        default: RES_LOOP(uint64_t, X(0) - 4 * X(1) + 6 * X(2) - 4 * X(3) + X(4)) break;
+        }
+    } else {
+        switch (k) {
+        case 0: RES_LOOP(uint32_t, X(0)) break;
+        case 1: RES_LOOP(uint32_t, X(0) - X(1)) break;
+        case 2: RES_LOOP(uint32_t, X(0) - 2 * X(1) + X(2)) break;
+        case 3: RES_LOOP(uint32_t, X(0) - 3 * X(1) + 3 * X(2) - X(3)) break;
+        default: RES_LOOP(uint32_t, X(0) - 4 * X(1) + 6 * X(2) - 4 * X(3) + X(4)) break;
         }
     }
+#undef RES_LOOP
+#undef X
 }
 
 /* ===================================================================== */
