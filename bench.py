@@ -5,10 +5,11 @@ metric : MSamples/s encoded (whole node), 44.1kHz/16-bit stereo, blocksize 4096
 unit   : 1 sample = one interchannel sample (STREAMINFO unit, metadata.zig:24)
 
 Workload (config 2).  S independent long streams (files) per GPU, encoded F
-4096-sample blocks of each per step (16384 streams x 8 blocks = 131072 blocks =
-2 GiB of PCM per step by default -- since round 3: 6 % above 65536-block steps on the same box,
-the persistent grids' ramp-down and the MD5 chain's tail amortised over twice the frames,
-profiles/r3r_shape.txt; the stream_curve field shows 8 .. 65536): the reference's per-file block loop
+4096-sample blocks of each per step (16384 streams x 16 blocks = 262144 blocks =
+4 GiB of PCM per step by default -- since round 3: per step the persistent grids' ramp-down and
+the MD5 chains' tail cost ~0.3 ms, amortised over more frames: 65536-block steps measured 6 %
+below 131072 (profiles/r3r_shape.txt), 131072 3.8 % below 262144 (profiles/r3x_shape.txt);
+the stream_curve field shows 8 .. 65536 streams at the same blocks per step): the reference's per-file block loop
 (wav2flac.zig:66-97) run for S files at once.  A step is one pass of the hot
 path over its batch: analysis (mid/side, wasted bits, fixed-order analysis,
 Rice search, subframe choice, exact frame sizes), frame-size scan, pack (bit
@@ -75,7 +76,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--frames", type=int, default=131072, help="4096-sample blocks per GPU per step")
+    p.add_argument("--frames", type=int, default=262144, help="4096-sample blocks per GPU per step")
     p.add_argument("--streams", type=int, default=16384, help="concurrent streams (files) per GPU")
     p.add_argument("--config", choices=sorted(PRESETS), default=None,
                    help="BASELINE.json config preset (overrides --channels/--bits/--rate/--lpc); default c2")
