@@ -123,6 +123,7 @@ struct flacgpu_ctx {
     int md5_engine = FLACGPU_MD5_HOST;
     int md5_kernel = 1;  // batched stream MD5: 1 = coalesced LDS-DMA ring, 0 = per-lane loads (A/B knob)
     int md5_prio = 0;    // issue priority of the MD5 waves beside the encode (A/B knob)
+    uint32_t enc_prio = 0;  // issue priority 1 for the C2 encode waves (A/B knob FLACGPU_ENC_PRIO)
     int md5_reserve = -1;  // 1: the analysis grid leaves one workgroup slot per stream-MD5 workgroup
                            //    queued beside it, 2: the pack grid too, 0: none, -1: auto (A/B knob)
     uint32_t grid_reserve = 0;  // per call: slots the next analysis / pack launches leave free
@@ -285,6 +286,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.image_bytes = c->image_bytes;
     a.stage_dbuf = c->stage_dbuf ? 1u : 0u;
     a.pack_dbuf = c->pack_dbuf ? 1u : 0u;
+    a.enc_prio = c->enc_prio;
     a.frame_bytes = d_fbytes;
     a.offsets = d_offsets;
     a.out = d_out;
@@ -618,6 +620,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (const char *e = std::getenv("FLACGPU_PACK_DBUF")) c->pack_dbuf = c->pack_dbuf && e[0] == '1';  // tuning knob
     if (const char *e = std::getenv("FLACGPU_MD5_KERNEL")) c->md5_kernel = std::atoi(e);  // A/B knob
     if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);      // A/B knob
+    if (const char *e = std::getenv("FLACGPU_ENC_PRIO")) c->enc_prio = e[0] == '1' ? 1u : 0u;  // A/B knob
     if (const char *e = std::getenv("FLACGPU_MD5_RESERVE")) c->md5_reserve = std::atoi(e);  // A/B knob
     if (const char *e = std::getenv("FLACGPU_MD5_DIAG")) c->md5_prio |= std::atoi(e) << 8;  // diagnostics
     // overlapped encode: ranges per call, workgroups per CU of the analysis / pack grids (A/B knobs)

@@ -144,6 +144,7 @@ struct EncodeArgs {
     uint32_t grid_per_cu;       // host side: at most this many persistent workgroups per CU (0 = as
                                 // many as fit) -- the overlapped encode shares each CU between an
                                 // analysis grid and a pack grid running on two streams
+    uint32_t enc_prio;          // A/B knob: the C2 encode waves at issue priority 1, above the MD5's 0
 };
 
 }  // namespace fg

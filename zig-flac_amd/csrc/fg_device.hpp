@@ -1179,6 +1179,7 @@ template <int B, int CLS, bool FULL, int MAXT, int NC, int LPW, bool FP = false>
 __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LPW == 0) ? FG_MINW
                                           : ((FULL && LPW > 0 && CLS == 24) ? 3 : 2)))
     k_analyze(EncodeArgs a) {
+    if (a.enc_prio) __builtin_amdgcn_s_setprio(1);
     using ST = typename Cls<CLS>::S;
     // LPC residuals may reach 2^30 in magnitude: 16-sample sums need 64 bits
     using SumT = typename std::conditional<LPW == 0, typename Cls<CLS>::Sum, uint64_t>::type;

@@ -69,6 +69,7 @@ __device__ __forceinline__ void p4_dsc_dma(const EncodeArgs &a, uint32_t slot, u
 
 template <int MAXT>
 __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
+    if (a.enc_prio) __builtin_amdgcn_s_setprio(1);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
     const uint32_t tid = threadIdx.x, NT = blockDim.x, NW = NT >> 6;
