@@ -26,9 +26,17 @@ compared byte for byte with the CPU restatement (oracle/, with the same frame
 numbers), and their carried MD5 states are finalised on the device and compared
 with hashlib over the bytes they absorbed.  `output_ok` is that comparison.
 
-One process per GPU (torchrun for N > 1).  Streams are independent files, so
+One process per GPU.  `bench.py --gpus N` without WORLD_SIZE in the environment
+starts N fresh child processes itself (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT; the parent never touches the GPU and
+prints nothing: rank 0's JSON line is the only stdout line); under torchrun
+(WORLD_SIZE set) the process is one rank.  Streams are independent files, so
 ranks shard streams with no data-path collective (weak scaling); a barrier and
 a max-over-ranks reduction bracket the timed region.
+
+After the headline (config 2) the default run times BASELINE configs 3, 4 and
+5 as their own lines (`configs`: 65536-block steps, the same barrier + max over
+ranks, output compared with the oracle, CPU port per config at N = 1).
 
 The JSON line also carries:
   roofline      -- the dominant kernel (analysis, pack or MD5: the longest mean
@@ -64,6 +72,9 @@ METRIC = "MSamples/s encoded (whole node), 44.1kHz/16-bit stereo, blocksize 4096
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # BASELINE.json configs (channels, bits, rate, LPC max order); c2 is the headline metric's
 PRESETS = {"c2": (2, 16, 44100, 0), "c3": (2, 24, 96000, 8), "c4": (8, 24, 96000, 0), "c5": (2, 32, 192000, 12)}
+# CPU-baseline sample per config (blocks, P threads; the one-core run takes 1/8 of it): about
+# 1-4 s of wall per run on the box's 16 cores at the measured per-core rates
+CPU_FRAMES = {"c2": 98304, "c3": 49152, "c4": 16384, "c5": 32768}
 LIMITER = {  # what binds each kernel (measured, not the roofline it is priced on)
     "analyze": "VALU issue/latency (integer dependent chains per lane), not HBM",
     "pack": "LDS atomics + dependent bit-offset chains, not HBM",
@@ -98,6 +109,10 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-frames", type=int, default=98304, help="blocks in the CPU-baseline sample")
     p.add_argument("--cpu-threads", type=int, default=0, help="0: the CPU share (OMP_NUM_THREADS), capped at a socket")
+    p.add_argument("--configs", default="c3,c4,c5",
+                   help="other BASELINE configs timed as their own lines after the headline ('' = none)")
+    p.add_argument("--cfg-frames", type=int, default=65536, help="blocks per GPU per step of each --configs line")
+    p.add_argument("--cfg-steps", type=int, default=20)
     a = p.parse_args()
     if a.config:
         a.channels, a.bits, a.rate, a.lpc = PRESETS[a.config]
@@ -627,19 +642,245 @@ def cpu_baseline(buf, args):
 
 
 # ---------------------------------------------------------------------------------------------
+# roofline of one configuration's step, from HIP events (bench) + the committed PMC summary
+VALU_PEAK = 1024 * 0.5 * 2.4e9  # wave64 VALU instructions/s: 1024 SIMD-32s x 1 per 2 cycles x 2.4 GHz
+
+
+def roofline_of(args, kt, steps, pcm_bytes, out_bytes, ms_per_step, key):
+    """The step's roofline.  `bound` is the resource that binds (VALU issue: Sigma SQ_INSTS_VALU of
+    every kernel of the step / (VALU peak x step time), from the committed PMC of this workload);
+    achieved / peak / frac price the dominant kernel against HBM (the contract's figure, kept
+    beside it).  Every kernel's own figures are in `kernels`."""
+    per_launch = {name: (v[1] / v[0]) / 1e3 for name, v in kt.items() if v[0]}
+    # launches per step: 1, or the range count of the overlapped schedule (FLACGPU_OVERLAP)
+    lps = {name: max(1, round(v[0] / steps)) for name, v in kt.items() if v[0]}
+    # The encode kernels run in sequence on the step's stream (analysis -> scan -> pack), the MD5
+    # beside them on its own stream: while the MD5's chain is shorter than the encode path the
+    # dominant kernel is the longest encode kernel, otherwise the MD5.
+    path_s = sum(per_launch.get(k, 0.0) * lps.get(k, 1) for k in ("analyze", "analyze_tail", "scan", "pack"))
+    fused = "pack" not in per_launch and "analyze" in per_launch  # FLACGPU_FUSED: no pack launch
+    algo = {"analyze": pcm_bytes + (out_bytes if fused else 0), "pack": pcm_bytes + out_bytes, "md5": pcm_bytes}
+    algo = {k: v // lps.get(k, 1) for k, v in algo.items()}
+    valu_step, valu_src, valu_missing = 0.0, None, []
+
+    def kernel_roofline(k):
+        avg = per_launch[k]
+        ach = algo[k] / avg / 1e9
+        traffic, counters, src = read_pmc(key, k)
+        issue = None
+        if counters.get("SQ_INSTS_VALU"):
+            issue = {"valu_wave_instr_per_launch": counters["SQ_INSTS_VALU"], "peak_valu_wave_instr_per_s": VALU_PEAK,
+                     "valu_issue_frac": round(counters["SQ_INSTS_VALU"] / avg / VALU_PEAK, 4),
+                     "waves_per_launch": counters.get("SQ_WAVES"), "source": src}
+        return {"achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(avg * 1e3, 4),
+                "algorithmic_bytes_per_launch": algo[k], "traffic": traffic, "traffic_source": src,
+                "traffic_ratio": round(traffic / algo[k], 3) if traffic else None, "issue": issue}
+
+    for k in per_launch:
+        _, counters, src = read_pmc(key, k)
+        if counters.get("SQ_INSTS_VALU"):
+            valu_step += counters["SQ_INSTS_VALU"] * lps[k]
+            valu_src = src
+        elif k in ("analyze", "pack", "md5"):
+            valu_missing.append(k)
+    enc_k = [k for k in ("analyze", "pack") if k in per_launch]
+    md5_off_path = "md5" not in per_launch or per_launch["md5"] < path_s
+    dom = max(enc_k, key=lambda k: per_launch[k] * lps[k]) if md5_off_path else "md5"
+    rk = {k: kernel_roofline(k) for k in ("analyze", "pack", "md5") if k in per_launch}
+    achieved = algo[dom] / per_launch[dom] / 1e9
+    step_issue = round(valu_step / (VALU_PEAK * ms_per_step / 1e3), 4) if valu_step and not valu_missing else None
+    return {
+        "bound": "valu-issue",
+        "step_issue_frac": step_issue,
+        "step_issue_note": ("Sigma SQ_INSTS_VALU per launch x launches per step over every kernel of the step "
+                            f"({valu_src}) / ({VALU_PEAK:.4g} wave-instr/s x ms_per_step)" if step_issue is not None
+                            else f"no committed PMC summary for workload {key} (kernels {valu_missing})"),
+        "limiter": LIMITER[dom],
+        "kernel": {"analyze": "k_analyze<..., FP> (fused analysis + pack, 4096-sample frames)" if fused
+                   else "k_analyze (4096-sample frames)", "pack": "k_pack4 / k_packw / k_pack",
+                   "md5": "k_md5_streams_lds"}[dom],
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "hbm_frac": round(achieved / HBM_PEAK_GBS, 5),
+        "traffic": rk[dom]["traffic"],
+        "traffic_source": rk[dom]["traffic_source"],
+        "algorithmic_bytes_per_launch": algo[dom],
+        "avg_launch_ms": round(per_launch[dom] * 1e3, 4),
+        "launches": kt[dom][0],
+        "launches_per_step": lps[dom],
+        "encode_path_gbs": round((pcm_bytes + out_bytes) / path_s / 1e9, 2) if path_s > 0 else None,
+        "issue": rk[dom]["issue"],
+        "selection": "longest encode kernel on the step's critical path (the MD5 chain, "
+                     f"{per_launch.get('md5', 0) * 1e3:.3f} ms, runs beside the {path_s * 1e3:.3f}-ms encode path)"
+                     if md5_off_path else "the MD5 chain is longer than the encode path: it bounds the step",
+        "kernels": rk,
+    }
+
+
+def workload_text(args, F):
+    cfg = (args.config or "c2").upper()
+    return (f"{cfg}: {args.rate/1000:g}kHz {args.bits}-bit {args.channels}ch, blocksize 4096, "
+            f"{args.streams} concurrent streams/GPU x {F} blocks each per step "
+            f"({args.frames} blocks/step), frame numbers + per-stream MD5 state carried across "
+            "steps, " + (f"LPC orders 1..{args.lpc} + full subframe-type search" if args.lpc else "fixed prediction") +
+            (", MD5 off (diagnostic)" if args.no_md5 else ", MD5 on its own HIP stream beside the next step's encode"))
+
+
+def config_line(args, cfg, dist, rank, world, dev):
+    """One BASELINE config (c3 / c4 / c5) as its own timed line inside the default run: its preset,
+    65536-block steps, barrier + max over ranks, output compared with the oracle after timing, the
+    CPU port timed on rank 0 at N = 1 (one core, P cores, and fixed-only for the LPC configs)."""
+    import numpy as np
+    import torch
+
+    import flacgpu
+
+    sub = argparse.Namespace(**vars(args))
+    sub.config = cfg
+    sub.channels, sub.bits, sub.rate, sub.lpc = PRESETS[cfg]
+    sub.frames, sub.streams = args.cfg_frames, args.streams
+    sub.cpu_frames = CPU_FRAMES[cfg]
+    buf = build_input(sub, rank)
+    fb = sub.channels * (sub.bits // 8)
+    enc = flacgpu.Encoder(sub.channels, sub.bits, sub.rate, device=torch.cuda.current_device(),
+                          max_frames=sub.frames, lpc_order=sub.lpc)
+    d_pcm = torch.from_numpy(buf).to(dev)
+    F = sub.frames // sub.streams
+    w = Workload(enc, d_pcm, sub.streams, F, fb, dev, md5=not args.no_md5)
+    elapsed = run_timed(w, args.cfg_steps, args.warmup, dist)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kt = kernel_times(enc)
+    pcm_bytes = sub.frames * 4096 * fb
+    out_bytes = int(w.d_fb.cpu().numpy().astype(np.int64).sum())
+    ms = elapsed / args.cfg_steps * 1e3
+    ok, vinfo = verify(sub, w, buf, fb, min(args.verify_streams, 32), dev) if rank == 0 else (True, {})
+    w.close()
+    enc.close()
+    del d_pcm
+    torch.cuda.empty_cache()
+    line = None
+    if rank == 0:
+        line = {"config": cfg, "workload": workload_text(sub, F), "workload_key": workload_key(sub),
+                "value": round(sub.frames * 4096 * world * args.cfg_steps / elapsed / 1e6, 2), "unit": "MSamples/s",
+                "n_gpus": world, "steps": args.cfg_steps, "ms_per_step": round(ms, 4),
+                "kernel_ms_per_step": {k: round(v[1] / args.cfg_steps, 4) for k, v in kt.items() if v[0]},
+                "compression_ratio": round(out_bytes / pcm_bytes, 4),
+                "roofline": roofline_of(sub, kt, args.cfg_steps, pcm_bytes, out_bytes, ms, workload_key(sub)),
+                "output_ok": ok, "verified": vinfo, "cpu_baseline": None}
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(buf, sub)
+            line["vs_cpu_single_socket_estimate"] = (round(line["value"] / line["cpu_baseline"]["single_socket_estimate"], 1)
+                                                     if line["cpu_baseline"].get("single_socket_estimate") else None)
+    return line
+
+
+def visible_gpus() -> int:
+    """GPUs this process could use, counted in a child process: the launcher itself never loads
+    torch or touches the GPU (FLACGPU_BENCH_FAKE_GPUS overrides the count: CPU tests)."""
+    fake = os.environ.get("FLACGPU_BENCH_FAKE_GPUS")
+    if fake is not None:
+        return int(fake)
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def launch(args) -> int:
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: one fresh child process per rank
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, the same argv), the torchrun
+    convention without torchrun.  The parent makes no GPU call before, during or after, never execs,
+    and prints nothing on stdout: rank 0's JSON line is the run's only stdout line.  Fewer visible
+    GPUs than N is an error (one rank per GPU).  Returns the exit code (the first failing rank's)."""
+    import socket
+
+    n = args.gpus
+    have = visible_gpus()
+    if have < n:
+        print(f"bench.py --gpus {n}: {have} GPU(s) visible; one rank per GPU needs {n}", file=sys.stderr)
+        return 2
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc, live = 0, set(range(n))
+    while live:
+        for i in sorted(live):
+            c = procs[i].poll()
+            if c is None:
+                continue
+            live.discard(i)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c  # killed by signal -c
+                for j in live:  # a rank failed: the others would wait for it forever
+                    procs[j].terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def stub_worker(args):
+    """FLACGPU_BENCH_STUB=1 (CPU tests of the launcher): the rank plumbing of main() -- gloo process
+    group from the launcher's environment, barrier, max-over-ranks, rank 0's one JSON line -- with
+    no GPU and no encode."""
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)  # as in main(): gloo / RCCL banners go to stderr
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if os.environ.get("FLACGPU_BENCH_STUB_FAIL") == str(rank):
+        raise SystemExit(7)  # a rank that dies before the rendezvous (launcher test)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids = [None] * world
+    dist.all_gather_object(ids, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "-1")),
+                                 "pid": os.getpid(), "ppid": os.getppid()})
+    dist.barrier()
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        os.write(json_fd, (json.dumps({"metric": METRIC, "stub": True, "n_gpus": world, "ranks": ids,
+                                       "max_over_ranks": t.item(), "steps": args.steps,
+                                       "warmup": args.warmup}) + "\n").encode())
+    dist.destroy_process_group()
+
+
 def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch(args))
+    if os.environ.get("FLACGPU_BENCH_STUB") == "1":
+        return stub_worker(args)
     # the contract is ONE JSON line on stdout: libraries that print banners there (RCCL prints
     # its version at communicator init, on every rank) are moved to stderr at the fd level
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
-    args = parse()
+    # the host MD5 pool (end_to_end) sizes itself from FLACGPU_MD5_THREADS, else the cgroup quota /
+    # affinity mask: on the GPU box that mask is the whole machine, the share is OMP_NUM_THREADS
+    if "FLACGPU_MD5_THREADS" not in os.environ and os.environ.get("OMP_NUM_THREADS", "1") not in ("", "1"):
+        os.environ["FLACGPU_MD5_THREADS"] = os.environ["OMP_NUM_THREADS"]
     import numpy as np
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus not in (1, world):
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running {world} ranks", file=sys.stderr)
     dist = None
     if world > 1:
         import torch.distributed as dist_mod
@@ -669,49 +910,14 @@ def main():
         elapsed = float(t.item())
     samples_per_rank = args.frames * 4096
     value = samples_per_rank * world * args.steps / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel, from HIP events on its stream
     kt = kernel_times(enc)
     fbytes = w.d_fb.cpu().numpy().astype(np.int64)
     total_bytes = int(w.d_tot[0].item())
     pcm_bytes = args.frames * 4096 * fb
-    per_launch = {name: (v[1] / v[0]) / 1e3 for name, v in kt.items() if v[0]}
-    # launches per step: 1, or the range count of the overlapped schedule (FLACGPU_OVERLAP, each
-    # range's analysis / scan / pack is its own launch); bytes per launch scale with it
-    lps = {name: max(1, round(v[0] / args.steps)) for name, v in kt.items() if v[0]}
-    # The dominant kernel bounds the step: the encode kernels run in sequence on the step's stream
-    # (analysis -> scan -> pack), the MD5 beside them on its own stream.  While the MD5's chain is
-    # shorter than the encode path it is off the critical path, and the dominant kernel is the
-    # longest encode kernel; otherwise the MD5.  Every kernel's own roofline is in `kernels`.
-    path_s = sum(per_launch.get(k, 0.0) * lps.get(k, 1) for k in ("analyze", "analyze_tail", "scan", "pack"))
     key = workload_key(args)
-    # fused single-pass encode (k_analyze<..., FP>, fg_fused.hpp): no pack launch, the analysis
-    # kernel also writes the frames
-    fused = "pack" not in per_launch and "analyze" in per_launch
-    algo = {"analyze": pcm_bytes + (int(fbytes.sum()) if fused else 0), "pack": pcm_bytes + int(fbytes.sum()),
-            "md5": pcm_bytes}
-    algo = {k: v // lps.get(k, 1) for k, v in algo.items()}
-
-    def kernel_roofline(k):
-        avg = per_launch[k]
-        ach = algo[k] / avg / 1e9
-        traffic, counters, src = read_pmc(key, k)
-        issue = None
-        if counters.get("SQ_INSTS_VALU"):
-            peak = 1024 * 0.5 * 2.4e9  # wave64 VALU instructions/s: 1024 SIMDs x 1 per 2 cycles x 2.4 GHz
-            issue = {"valu_wave_instr_per_launch": counters["SQ_INSTS_VALU"], "peak_valu_wave_instr_per_s": peak,
-                     "valu_issue_frac": round(counters["SQ_INSTS_VALU"] / avg / peak, 4),
-                     "waves_per_launch": counters.get("SQ_WAVES"), "source": src}
-        return {"achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(avg * 1e3, 4),
-                "algorithmic_bytes_per_launch": algo[k], "traffic": traffic, "traffic_source": src, "issue": issue}
-
-    enc_k = [k for k in ("analyze", "pack") if k in per_launch]
-    md5_off_path = "md5" not in per_launch or per_launch["md5"] < path_s
-    dom = max(enc_k, key=lambda k: per_launch[k] * lps[k]) if md5_off_path else "md5"
-    rk = {k: kernel_roofline(k) for k in ("analyze", "pack", "md5") if k in per_launch}
-    algo_bytes, avg_s = algo[dom], per_launch[dom]
-    achieved = algo_bytes / avg_s / 1e9
-    traffic, pmc_src, issue = rk[dom]["traffic"], rk[dom]["traffic_source"], rk[dom]["issue"]
+    roof = roofline_of(args, kt, args.steps, pcm_bytes, int(fbytes.sum()), ms_per_step, key)
 
     ok, vinfo = verify(args, w, buf, fb, args.verify_streams, dev) if rank == 0 else (True, {})
     w.close()
@@ -734,6 +940,15 @@ def main():
             e2e = end_to_end(args)
         if not args.no_cpu:
             cpu = cpu_baseline(buf, args)
+    d_pcm = None
+    enc.close()
+    torch.cuda.empty_cache()
+
+    # the other BASELINE configs, each its own timed line (every rank: streams sharded as above)
+    configs = None
+    if args.configs and not args.config:
+        del buf
+        configs = [config_line(args, c, dist, rank, world, dev) for c in args.configs.split(",") if c]
 
     if e2e and cpu:
         e2e["vs_cpu_measured_P_cores"] = round(e2e["value"] / cpu["value"], 2)
@@ -741,7 +956,6 @@ def main():
             e2e["vs_cpu_single_socket_estimate"] = round(e2e["value"] / cpu["single_socket_estimate"], 2)
 
     if rank == 0:
-        cfg = (args.config or "c2").upper()
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -749,53 +963,27 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
             "config": {
-                "workload": f"{cfg}: {args.rate/1000:g}kHz {args.bits}-bit {args.channels}ch, blocksize 4096, "
-                            f"{args.streams} concurrent streams/GPU x {F} blocks each per step "
-                            f"({args.frames} blocks/step), frame numbers + per-stream MD5 state carried across "
-                            "steps, " + (f"LPC orders 1..{args.lpc} + full subframe-type search"
-                                         if args.lpc else "fixed prediction") +
-                            (", MD5 off (diagnostic)" if args.no_md5 else
-                             ", MD5 on its own HIP stream beside the next step's encode"),
+                "workload": workload_text(args, F),
                 "workload_key": key,
                 "blocks_per_gpu_per_step": args.frames,
                 "streams_per_gpu": args.streams,
                 "samples_per_gpu_per_step": samples_per_rank,
                 "compression_ratio": round(total_bytes / pcm_bytes, 4),
                 "parallelism": f"streams sharded over {world} GPU(s), no collective on the data path",
+                "launcher": "torchrun / bench.py --gpus N (one fresh process per rank)" if world > 1 else "one process",
             },
-            "roofline": {
-                "bound": "hbm",
-                "limiter": LIMITER[dom],
-                "kernel": {"analyze": "k_analyze<..., FP> (fused analysis + pack, 4096-sample frames)" if fused
-                           else "k_analyze (4096-sample frames)", "pack": "k_pack4 / k_packw / k_pack",
-                           "md5": "k_md5_streams_lds"}[dom],
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
-                "traffic_source": pmc_src,
-                "algorithmic_bytes_per_launch": algo_bytes,
-                "avg_launch_ms": round(avg_s * 1e3, 4),
-                "launches": kt[dom][0],
-                "launches_per_step": lps[dom],
-                "encode_path_gbs": round((pcm_bytes + int(fbytes.sum())) / path_s / 1e9, 2) if path_s > 0 else None,
-                "issue": issue,
-                "selection": "longest encode kernel on the step's critical path (the MD5 chain, "
-                             f"{per_launch.get('md5', 0) * 1e3:.3f} ms, runs beside the {path_s * 1e3:.3f}-ms encode path)"
-                             if md5_off_path else "the MD5 chain is longer than the encode path: it bounds the step",
-                "kernels": rk,
-            },
+            "roofline": roof,
             "kernel_ms_per_step": {k: round(v[1] / args.steps, 4) for k, v in kt.items() if v[0]},
             "output_ok": ok,
             "verified": vinfo,
+            "configs": configs,
             "stream_curve": curve,
             "sharded_stream": sharded,
             "end_to_end": e2e,
@@ -803,7 +991,6 @@ def main():
         }
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(line) + "\n").encode())
-    enc.close()
     if dist:
         dist.destroy_process_group()
 

@@ -1,8 +1,12 @@
 // The host hashing pool (fg_md5_host.cpp md5_pool_update) against one plain HostMd5 chain per
 // message: many caller threads at once, ragged lengths, updates split at odd offsets (partial
-// blocks carried), worker counts from FLACGPU_MD5_THREADS.  Prints "ok" or the first mismatch.
+// blocks carried), worker counts from FLACGPU_MD5_THREADS, and a forked child (the pool's workers
+// do not exist there: the child must hash on its own thread, not wait forever for them).
+// Prints "ok" or the first mismatch.
 #include <stdio.h>
 #include <string.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <random>
 #include <thread>
@@ -44,6 +48,22 @@ int main() {
                 printf("mismatch: round %d message %d (%zu bytes)\n", round, i, msgs[i].size());
                 return 1;
             }
+    }
+    // fork after the pool's workers started: the child hashes inline (no worker threads exist in
+    // it); a child that queued its job would block forever, so the parent bounds the wait
+    const pid_t pid = fork();
+    if (pid == 0) {
+        alarm(20);
+        fg::HostMd5 h;
+        fg::md5_pool_update(&h, msgs[1].data(), msgs[1].size());
+        std::array<uint8_t, 16> d;
+        h.final(d.data());
+        _exit(memcmp(d.data(), want[1].data(), 16) == 0 ? 0 : 3);
+    }
+    int st = 0;
+    if (pid < 0 || waitpid(pid, &st, 0) != pid || !WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+        printf("forked child failed (status %d)\n", st);
+        return 1;
     }
     printf("ok\n");
     return 0;

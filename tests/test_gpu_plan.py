@@ -364,3 +364,45 @@ def test_overlapped_schedule_many_ranges_and_serial_again():
             res, _ = _run_plan(enc, bytes(buf), offs, lengths, md5="none")
             for s, (got, sizes, _) in enumerate(res):
                 assert (got, sizes) == (refs[s][0], refs[s][1]), f"ranges {ranges} stream {s}"
+
+
+def _host_replay(sizes, lo=0xFFFFFF, hi=0):
+    """StreamInfo.updateFrameSize (metadata.zig:35-40) through the C ABI's host restatement."""
+    import flacgpu
+
+    si = flacgpu.StreamInfo.new(44100, 2, 16, 0)
+    si.min_frame_size, si.max_frame_size = lo, hi
+    for v in sizes:
+        si.update_frame_size(int(v))
+    return [int(si.min_frame_size), int(si.max_frame_size)]
+
+
+@pytest.mark.parametrize("n", [1, 64, 1023, 1025, 5000, 70000])
+@pytest.mark.parametrize("shape", ["random", "rising", "falling", "sawtooth"])
+@pytest.mark.parametrize("carried", [False, True])
+def test_streaminfo_replay_device_matches_host(n, shape, carried):
+    """flacgpu_streaminfo_replay_device (k_streaminfo_replay: per-thread runs past 1024 frames,
+    cross-wave max scan with a carried {min, max}) == the host loop of
+    flacgpu_streaminfo_update_frame_size, including the reference's else-if quirk (a frame that
+    raises the running max never lowers the min)."""
+    import flacgpu
+
+    torch, dev = _torch()
+    rng = np.random.default_rng(n * 7 + len(shape))
+    if shape == "random":
+        sizes = rng.integers(10, 20000, n)
+    elif shape == "rising":
+        sizes = np.arange(n) * 3 + 100
+    elif shape == "falling":
+        sizes = 400000 - np.arange(n) * 5
+    else:
+        sizes = (np.arange(n) % 97) * 11 + rng.integers(0, 3, n)
+    sizes = sizes.astype(np.int32)
+    start = [1500, 9000] if carried else [0xFFFFFF, 0]
+    want = _host_replay(sizes, *start)
+    with flacgpu.Encoder(2, 16, 44100, device=0, max_frames=64) as enc:
+        d_fb = torch.from_numpy(sizes).to(dev)
+        mm = torch.tensor(start, dtype=torch.int32, device=dev)
+        enc.streaminfo_replay_device(d_fb.data_ptr(), n, mm.data_ptr())
+        torch.cuda.synchronize()
+        assert mm.cpu().tolist() == want

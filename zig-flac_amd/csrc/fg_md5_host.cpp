@@ -2,8 +2,10 @@
 #include "fg_md5_host.hpp"
 
 #include <sched.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -161,7 +163,9 @@ class Md5Pool {
             p += take;
             len -= take;
         }
-        if (h->fill || len < 64u * 64u || workers_ == 0) {  // short updates: no hand-off
+        // short updates, no workers, or a forked child (the pool's threads live only in the
+        // process that created them): the caller hashes its own chain
+        if (h->fill || len < 64u * 64u || workers_ == 0 || getpid() != owner_) {
             h->update(p, len);
             return;
         }
@@ -184,19 +188,28 @@ class Md5Pool {
   private:
     static constexpr int kMaxChains = 4;
     static constexpr size_t kChunk = 256;  // blocks per chain between queue checks
-    Md5Pool() {
+    // The process's CPU share: the cgroup v2 quota where one is set (it is not visible in the
+    // affinity mask), else the affinity mask.  Not OMP_NUM_THREADS: launchers such as torchrun
+    // set it to 1 per process, which would put every file's chain on one worker.
+    static int cpu_share() {
+        int n = 0;
+        if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {};
+            long long period = 0;
+            if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+                const long long quota = atoll(q);
+                if (quota > 0) n = (int)((quota + period - 1) / period);
+            }
+            fclose(f);
+        }
+        cpu_set_t set;
+        const int aff = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+        return (n > 0 && n < aff) ? n : aff;
+    }
+    Md5Pool() : owner_(getpid()) {
         int n = 0;
         if (const char *e = std::getenv("FLACGPU_MD5_THREADS")) n = std::atoi(e);  // < 0: no pool (A/B)
-        if (n == 0) {
-            // the CPU share: OMP_NUM_THREADS where the environment states it (a cgroup quota is
-            // not visible in the affinity mask), else the affinity mask; the callers mostly wait
-            // on the GPU
-            if (const char *e = std::getenv("OMP_NUM_THREADS")) n = std::atoi(e);
-            if (n <= 0) {
-                cpu_set_t set;
-                n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
-            }
-        }
+        if (n == 0) n = cpu_share();  // the callers mostly wait on the GPU
         if (n > 64) n = 64;
         if (n < 0) n = 0;  // every caller hashes its own chain
         for (int i = 0; i < n; i++) {
@@ -258,6 +271,7 @@ class Md5Pool {
     std::condition_variable cv_, done_cv_;
     std::deque<Md5Job *> q_;
     int workers_ = 0, idle_ = 0;
+    const pid_t owner_;  // the process whose workers these are
 };
 
 }  // namespace

@@ -429,7 +429,9 @@ class Encoder:
                               d_frame_offsets: int, d_total: int, d_md5_state: Optional[int] = None,
                               d_md5: Optional[int] = None, stream: Optional[int] = None,
                               md5_stream: Optional[int] = None) -> None:
-        """flacgpu_encode_plan_device_ex: MD5 state carried in d_md5_state (32 B per stream)."""
+        """flacgpu_encode_plan_device_ex: MD5 state carried in d_md5_state (32 B per stream).
+        md5_stream None: the MD5 is joined back into `stream`; any handle (0 = the legacy null
+        stream) queues it there unjoined, as in encode_plan_device."""
         _check(self.lib.flacgpu_encode_plan_device_ex(
             self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total,
             d_md5_state or None, d_md5 or None, _stream(stream), _stream(md5_stream)), "encode_plan_device_ex")
@@ -470,8 +472,10 @@ class Encoder:
                            d_frame_offsets: int, d_total: int, d_md5: Optional[int] = None,
                            stream: Optional[int] = None, md5_stream: Optional[int] = None) -> None:
         """md5_stream: queue the MD5 there without joining it back into `stream` (the caller
-        synchronises it); None joins it (flacgpu_encode_plan_device)."""
-        if md5_stream:
+        synchronises it); None joins it (flacgpu_encode_plan_device).  As in encode_plan_device_ex,
+        only None means "joined": a handle of 0 is the legacy null stream (_stream), like any
+        other stream handle."""
+        if md5_stream is not None:
             _check(self.lib.flacgpu_encode_plan_device_md5_async(
                 self.ctx, plan.handle, d_pcm, d_out, out_cap, d_frame_bytes, d_frame_offsets, d_total,
                 d_md5 or None, _stream(stream), _stream(md5_stream)), "encode_plan_device_md5_async")

@@ -147,7 +147,12 @@ class ShardedStream:
 
     def step(self, pcm):
         """Encode this rank's shard of the next window; rank 0 returns (bitstream, sizes) of the
-        whole window (tensors on the communication device), other ranks None."""
+        whole window (tensors on the communication device), other ranks None.
+
+        With the GPU encoder the returned tensors are VIEWS of this object's receive buffers: the
+        next step() encodes and gathers into the same memory, so they are valid only until then.
+        A caller that keeps a window (appends it to a list, hands it to another thread) must
+        .clone() or .cpu() it first."""
         import numpy as np
         import torch
 
