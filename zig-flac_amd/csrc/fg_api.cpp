@@ -135,6 +135,8 @@ struct flacgpu_ctx {
     // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp): analysis and pack in
     // one kernel, frame offsets by an in-kernel look-back over per-slot status words
     bool fused = false;
+    // one wave per full 16-bit stereo frame (fg_ana1.hpp k_ana1) instead of one per candidate
+    bool ana1 = false;
     uint32_t lds_fused = 0, crc_hmaxf = 0;
     uint16_t *d_crc_powf = nullptr;  // CRC fold shifts for its 256 threads
     uint64_t *d_status = nullptr;    // per-slot status words, grow-only
@@ -317,6 +319,8 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
             h.xcd_queue = c->xcd_queue ? 1u : 0u;
             HIPCHK(launch_stage(0, h, true, c->nt_split, c->lds_split, s));
             HIPCHK(launch_frame_totals(h, s));
+        } else if (c->ana1) {
+            HIPCHK(launch_stage(3, h, true, 64u, (uint32_t)Ana1Layout::total, s));
         } else {
             HIPCHK(launch_stage(0, h, true, c->nt, c->lds, s));
         }
@@ -675,6 +679,8 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         }
     }
     if (c->C == 2 && c->B == 2 && !lpc && c->stereo) {
+        c->ana1 = true;
+        if (const char *e = std::getenv("FLACGPU_ANA1")) c->ana1 = e[0] != '0';  // A/B knob
         c->fused = false;
         if (const char *e = std::getenv("FLACGPU_FUSED")) c->fused = e[0] == '1';  // A/B knob
         c->lds_fused = ana_layout(2, 2, 4, true, false, false, c->image_bytes).total;

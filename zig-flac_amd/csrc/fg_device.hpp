@@ -2501,6 +2501,7 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
 
 #include "fg_pack4.hpp"
 #include "fg_packw.hpp"
+#include "fg_ana1.hpp"
 
 // persistent launch: grid = min(work items, resident workgroups on this device).  The occupancy
 // is cached per (kernel, threads, LDS, device); the lock covers only the cache lookup/insert, so
@@ -2574,8 +2575,11 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
         // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp)
         if (stage == 2 && full && a.channels == 2 && a.stereo && threads == 256u)
             return launch_persistent(k_analyze<2, 16, true, 256, 2, 0, true>, a, threads, lds, st);
+        // one wave per full 16-bit stereo frame (fg_ana1.hpp)
+        if (stage == 3 && full && a.channels == 2 && a.stereo && threads == 64u)
+            return launch_persistent(k_ana1<1>, a, threads, lds, st);
     }
-    if (stage == 2) return hipErrorInvalidValue;
+    if (stage >= 2) return hipErrorInvalidValue;
     // other full frames: WPS waves per written subframe (fg_packw.hpp); the host marks it by
     // the thread count 64 * n_out * WPS (k_pack runs 64 * n_out)
     if (stage == 1 && full && a.ch_split) {

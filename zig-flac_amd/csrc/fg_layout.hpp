@@ -95,6 +95,13 @@ __host__ __device__ inline PackLayout pack_layout(uint32_t C, uint32_t B, uint32
     return L;
 }
 
+// k_ana1 (fg_ana1.hpp, one wave per frame): per-wave LDS of the four candidates' Rice parameters
+// (512 B each, orders 0..8 at (1 << o) - 1), their decisions (8 u32 each), the frame header words
+// (4) and its byte count.
+struct Ana1Layout {
+    static constexpr uint32_t par = 0, rec = 2048, hdr = 2048 + 128, total = 2048 + 128 + 32;
+};
+
 // k_pack4 (fg_pack4.hpp): two staging / image buffers, scratch, and two LDS copies of a frame
 // descriptor (320 dwords each, DMA'd a frame ahead)
 struct P4Layout {
