@@ -58,40 +58,28 @@ __device__ __forceinline__ int32_t cand_x(uint32_t w) {
     else return L - R;
 }
 
-// The candidate sample of a packed word in SDWA form (sign-extended 16-bit halves as operands):
-// L and R one op with the bias folded in, side one op, mid two.  Returns the sample; *b0 = sample +
-// 0x7FFFFFFF (kb: that constant in a VGPR).
+// The candidate sample of a packed word; the compiler forms SDWA operations (sign-extended 16-bit
+// halves as operands): L and R one v_add_u32_sdwa with the bias folded in, side two ops, mid two
+// (the sum kept opaque: otherwise (L + R) >> 1 is narrowed to a five-op 16-bit average).  Inline
+// asm is avoided here: the hazard recognizer pads every asm statement with s_nop.  Returns the
+// sample; *b0 = sample + 0x7FFFFFFF.
 template <int CAND>
 __device__ __forceinline__ int32_t cand_sdwa(uint32_t w, uint32_t kb, uint32_t *b0) {
+    const int32_t L = (int32_t)(w << 16) >> 16, R = (int32_t)w >> 16;
     int32_t x;
-    if constexpr (CAND == 0) {
-        asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD"
-            : "=v"(*b0) : "v"(w), "v"(kb));
-        x = (int32_t)(*b0 - kb);
-    } else if constexpr (CAND == 1) {
-        asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
-            : "=v"(*b0) : "v"(w), "v"(kb));
-        x = (int32_t)(*b0 - kb);
-    } else if constexpr (CAND == 2) {
-        int32_t t;
-        asm("v_add_u32_sdwa %0, sext(%1), sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
-            : "=v"(t) : "v"(w));
+    if constexpr (CAND == 0) x = L;
+    else if constexpr (CAND == 1) x = R;
+    else if constexpr (CAND == 2) {
+        int32_t t = L + R;
+        asm volatile("" : "+v"(t));
         x = t >> 1;
-        *b0 = (uint32_t)x + kb;
-    } else {
-        asm("v_sub_u32_sdwa %0, sext(%1), sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
-            : "=v"(x) : "v"(w));
-        *b0 = (uint32_t)x + kb;
-    }
+    } else x = L - R;
+    *b0 = (uint32_t)x + kb;
     return x;
 }
 
-// v_mad_i32_i24: a * b + c on 24-bit signed operands (full rate; v_mul_lo_u32 is quarter rate)
-__device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c) {
-    int32_t d;
-    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
-    return d;
-}
+// a * b + c on 24-bit signed operands: v_mad_i32_i24 (full rate; v_mul_lo_u32 is quarter rate)
+__device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c) { return __mul24(a, b) + c; }
 
 __device__ __forceinline__ uint32_t max3_u32(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t d;
@@ -136,7 +124,7 @@ __device__ __forceinline__ void pass1(const uint32_t (&rq)[64], uint32_t l, Pass
     uint32_t pb3 = (u1 - 3u * u2 + 3u * u3 - u4) + KB;
     uint32_t ov = 0;
     const bool z = (l == 0);
-    const uint32_t kbv = opaque(KB);  // (a VGPR operand of the SDWA forms)
+    const uint32_t kbv = KB;
 #pragma unroll
     for (int g = 0; g < 4; g++) {
         uint32_t S0 = 0, S1 = 0, S2 = 0, S3 = 0, S4 = 0;
