@@ -6,4 +6,4 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_pl
 rc=$?
 echo "parity rc=$rc"; tail -3 gpurun_out/r4b_parity.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-AB_REPS=2 tools/ab.sh r4b c2 one:FLACGPU_ANA1=1 four:FLACGPU_ANA1=0
+AB_REPS=2 tools/ab.sh r4b c2 v1:FLACGPU_ANA1=1 v2:FLACGPU_ANA1=2 four:FLACGPU_ANA1=0
