@@ -137,6 +137,7 @@ struct flacgpu_ctx {
     bool fused = false;
     // one wave per full 16-bit stereo frame (fg_ana1.hpp k_ana1) instead of one per candidate
     bool ana1 = false;
+    uint32_t ana1_variant = 1;
     uint32_t lds_fused = 0, crc_hmaxf = 0;
     uint16_t *d_crc_powf = nullptr;  // CRC fold shifts for its 256 threads
     uint64_t *d_status = nullptr;    // per-slot status words, grow-only
@@ -289,6 +290,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
     a.stage_dbuf = c->stage_dbuf ? 1u : 0u;
     a.pack_dbuf = c->pack_dbuf ? 1u : 0u;
     a.enc_prio = c->enc_prio;
+    a.ana1_variant = c->ana1_variant;
     a.frame_bytes = d_fbytes;
     a.offsets = d_offsets;
     a.out = d_out;
@@ -680,7 +682,10 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     }
     if (c->C == 2 && c->B == 2 && !lpc && c->stereo) {
         c->ana1 = true;
-        if (const char *e = std::getenv("FLACGPU_ANA1")) c->ana1 = e[0] != '0';  // A/B knob
+        if (const char *e = std::getenv("FLACGPU_ANA1")) {  // A/B knob: 0 = k_analyze, 1 / 2 = k_ana1 variant
+            c->ana1 = e[0] != '0';
+            c->ana1_variant = e[0] == '2' ? 2u : 1u;
+        }
         c->fused = false;
         if (const char *e = std::getenv("FLACGPU_FUSED")) c->fused = e[0] == '1';  // A/B knob
         c->lds_fused = ana_layout(2, 2, 4, true, false, false, c->image_bytes).total;

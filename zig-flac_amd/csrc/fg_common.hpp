@@ -145,6 +145,7 @@ struct EncodeArgs {
                                 // many as fit) -- the overlapped encode shares each CU between an
                                 // analysis grid and a pack grid running on two streams
     uint32_t enc_prio;          // A/B knob: the C2 encode waves at issue priority 1, above the MD5's 0
+    uint32_t ana1_variant;      // k_ana1 register budget (fg_ana1.hpp): 1 = 3 waves/SIMD, 2 = 4
 };
 
 }  // namespace fg

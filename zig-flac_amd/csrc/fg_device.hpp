@@ -2577,7 +2577,8 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
             return launch_persistent(k_analyze<2, 16, true, 256, 2, 0, true>, a, threads, lds, st);
         // one wave per full 16-bit stereo frame (fg_ana1.hpp)
         if (stage == 3 && full && a.channels == 2 && a.stereo && threads == 64u)
-            return launch_persistent(k_ana1<1>, a, threads, lds, st);
+            return a.ana1_variant == 2 ? launch_persistent(k_ana1<2>, a, threads, lds, st)
+                                       : launch_persistent(k_ana1<1>, a, threads, lds, st);
     }
     if (stage >= 2) return hipErrorInvalidValue;
     // other full frames: WPS waves per written subframe (fg_packw.hpp); the host marks it by
