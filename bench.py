@@ -122,7 +122,10 @@ def parse():
 def workload_key(a) -> str:
     # the fused single-pass schedule (FLACGPU_FUSED=1) runs other kernels: its own PMC summaries
     fused = os.environ.get("FLACGPU_FUSED", "0") == "1"
-    return f"{a.config or 'c2'}:{a.frames}x{a.streams}" + ("+fused" if fused else "")
+    # the one-wave-per-frame C2 analysis (FLACGPU_ANA1=1 / 2, fg_ana1.hpp) likewise
+    ana1 = os.environ.get("FLACGPU_ANA1", "0")
+    return (f"{a.config or 'c2'}:{a.frames}x{a.streams}" + ("+fused" if fused else "") +
+            (f"+ana1v{ana1}" if ana1 in ("1", "2") and (a.config or "c2") == "c2" else ""))
 
 
 def build_input(args, rank):

@@ -16,7 +16,7 @@ mkdir -p gpurun_out
 SUM=gpurun_out/ab_$TAG.txt
 REPS=${AB_REPS:-2}
 for cfg in $CFGS; do
-  CA="--configs ''"; ST=${AB_STEPS:-20}
+  CA="--configs="; ST=${AB_STEPS:-20}
   if [ "$cfg" != c2 ]; then CA="--config $cfg"; ST=${AB_STEPS:-10}; fi
   for rep in $(seq $REPS); do
     for V in "$@"; do

@@ -16,7 +16,7 @@ import re
 import sys
 from collections import defaultdict
 
-FAMILIES = [("analyze_tail", r"k_analyze<\d+, \d+, false"), ("analyze", r"k_analyze<\d+, \d+, true"), ("analyze", r"k_ana4<"),
+FAMILIES = [("analyze_tail", r"k_analyze<\d+, \d+, false"), ("analyze", r"k_analyze<\d+, \d+, true"), ("analyze", r"k_ana4<"), ("analyze", r"k_ana1<"),
             ("pack_tail", r"k_pack<\d+, \d+, false"), ("pack", r"k_pack<\d+, \d+, true"), ("pack", r"k_pack4<"), ("pack", r"k_packw<"),
             ("scan", r"k_scan"), ("md5", r"k_md5_streams"), ("md5_blocks", r"k_md5_blocks")]
 

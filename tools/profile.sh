@@ -10,7 +10,7 @@ TAG=${1:-r2}; shift || true
 CFG=${1:-c2}; shift || true
 FRAMES=${1:-65536}; shift || true
 STREAMS=${1:-16384}; shift || true
-ARGS="--config $CFG --frames $FRAMES --streams $STREAMS --steps 5 --warmup 2 --no-cpu --no-curve --no-e2e --no-sharded --verify-streams 4 $@"
+ARGS="--config $CFG --frames $FRAMES --streams $STREAMS --steps 5 --warmup 2 --no-cpu --no-curve --no-e2e --no-sharded --configs= --verify-streams 4 $@"
 REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p $OUT
@@ -22,7 +22,10 @@ for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_IN
   timeout -s KILL 180 rocprofv3 --pmc $PMC --output-format csv -d $OUT/pmc$i -o pmc -- python3 $REPO/bench.py $ARGS > $OUT/pmc$i.log 2>&1 || { echo "PMC pass $i ($PMC) failed: no further GPU passes"; break; }
 done
 cd $REPO
-python3 tools/pmc_summary.py $OUT $TAG $FRAMES "$CFG:${FRAMES}x${STREAMS}"
+KEY="$CFG:${FRAMES}x${STREAMS}"  # bench.py workload_key
+[ "${FLACGPU_FUSED:-0}" = 1 ] && KEY="$KEY+fused"
+case "${FLACGPU_ANA1:-0}" in 1|2) [ "$CFG" = c2 ] && KEY="$KEY+ana1v$FLACGPU_ANA1" ;; esac
+python3 tools/pmc_summary.py $OUT $TAG $FRAMES "$KEY"
 cp $OUT/kt/kt_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
 # profiles/ does not travel back from the GPU box: mirror the summaries under gpurun_out/
 mkdir -p $REPO/gpurun_out/profiles && cp profiles/${TAG}_* $REPO/gpurun_out/profiles/

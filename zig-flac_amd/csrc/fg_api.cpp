@@ -681,7 +681,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         }
     }
     if (c->C == 2 && c->B == 2 && !lpc && c->stereo) {
-        c->ana1 = true;
+        c->ana1 = false;  // measured slower than k_analyze so far: opt-in
         if (const char *e = std::getenv("FLACGPU_ANA1")) {  // A/B knob: 0 = k_analyze, 1 / 2 = k_ana1 variant
             c->ana1 = e[0] != '0';
             c->ana1_variant = e[0] == '2' ? 2u : 1u;
