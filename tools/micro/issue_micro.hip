@@ -1,0 +1,83 @@
+// issue_micro.hip -- VALU issue throughput on gfx950 for the integer forms the analysis kernels
+// are built from (tools only): v_add_u32, v_sad_u32, v_xad_u32, v_max3_u32, v_add_u32_sdwa,
+// v_mul_u32_u24, at 1..8 waves per SIMD, 8 independent chains per lane.  Reports wave-instructions
+// per SIMD-cycle from the in-kernel clock (s_memtime / s_memrealtime x 100 MHz), so DVFS is
+// factored out: 0.5 = one wave64 VALU instruction every 2 cycles (the SIMD-32 peak).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+template <int KIND>
+__global__ void __launch_bounds__(64) k(const unsigned *in, unsigned *out, unsigned long long *clk, int iters) {
+    const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { a[i] = in[(t + 8 * i) & 1023]; b[i] = in[(t * 3 + i) & 1023]; }
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const unsigned x = b[(i + r) & 7];
+                // inline asm: one instruction each, nothing folded across the unrolled loop
+                if constexpr (KIND == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 1) asm volatile("v_sad_u32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(x), "v"(b[i]));
+                else if constexpr (KIND == 2) asm volatile("v_xad_u32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(x), "v"(b[i]));
+                else if constexpr (KIND == 3) asm volatile("v_max3_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(x), "v"(b[i]));
+                else if constexpr (KIND == 4)
+                    asm volatile("v_add_u32_sdwa %0, sext(%1), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD"
+                                 : "+v"(a[i]) : "v"(x));
+                else asm volatile("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(a[i]) : "v"(x), "v"(b[i]));
+            }
+        b[0] ^= a[7];
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    unsigned s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s ^= a[i];
+    out[t] = s;
+    if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
+}
+
+template <int KIND>
+void run(const char *name, unsigned *din, unsigned *dout, unsigned long long *dclk, int wps) {
+    const int cus = 256, blocks = cus * 4 * wps, iters = 2000;
+    hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(64), 0, 0, din, dout, dclk, 10);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(64), 0, 0, din, dout, dclk, iters);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    unsigned long long clk[2];
+    (void)hipMemcpy(clk, dclk, 16, hipMemcpyDeviceToHost);
+    const double ghz = (double)clk[0] / ((double)clk[1] / 100e6) / 1e9;  // in-kernel clock
+    const double instr = (double)blocks * iters * 16 * 8;                 // wave-instructions (ops per lane)
+    const double per_simd_cycle = instr / (cus * 4.0) / (ms * 1e-3 * ghz * 1e9);
+    printf("%-10s waves/SIMD %d: %.3f ms, clock %.2f GHz, %.3f wave-instr per SIMD-cycle\n", name, wps, ms, ghz,
+           per_simd_cycle);
+}
+
+int main() {
+    unsigned *din, *dout;
+    unsigned long long *dclk;
+    (void)hipMalloc(&din, 4096 * 4);
+    (void)hipMalloc(&dout, 256 * 4 * 8 * 64 * 4);
+    (void)hipMalloc(&dclk, 16);
+    unsigned h[1024];
+    for (int i = 0; i < 1024; i++) h[i] = rand();
+    (void)hipMemcpy(din, h, 4096, hipMemcpyHostToDevice);
+    for (int w : {1, 2, 3, 4, 8}) {
+        run<0>("v_add", din, dout, dclk, w);
+        run<1>("v_sad", din, dout, dclk, w);
+        run<2>("v_xad", din, dout, dclk, w);
+        run<3>("v_max3", din, dout, dclk, w);
+        run<4>("add_sdwa", din, dout, dclk, w);
+        run<5>("mad_u24", din, dout, dclk, w);
+    }
+    return 0;
+}
