@@ -11,6 +11,7 @@ template <int KIND>
 __global__ void __launch_bounds__(64) k(const unsigned *in, unsigned *out, unsigned long long *clk, int iters) {
     const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned a[8], b[8];
+    const unsigned kk = (unsigned)__builtin_amdgcn_readfirstlane((int)in[5]);
 #pragma unroll
     for (int i = 0; i < 8; i++) { a[i] = in[(t + 8 * i) & 1023]; b[i] = in[(t * 3 + i) & 1023]; }
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -28,7 +29,16 @@ __global__ void __launch_bounds__(64) k(const unsigned *in, unsigned *out, unsig
                 else if constexpr (KIND == 4)
                     asm volatile("v_add_u32_sdwa %0, sext(%1), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD"
                                  : "+v"(a[i]) : "v"(x));
-                else asm volatile("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(a[i]) : "v"(x), "v"(b[i]));
+                else if constexpr (KIND == 5) asm volatile("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(a[i]) : "v"(x), "v"(b[i]));
+                // encoding vs operand count: VOP3 forms with two VGPR sources, VOP2 forms
+                else if constexpr (KIND == 6) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 7) asm volatile("v_sad_u32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(x), "s"(kk));
+                else if constexpr (KIND == 8) asm volatile("v_xad_u32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(x), "s"(kk));
+                else if constexpr (KIND == 9) asm volatile("v_max_u32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 10) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 11) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(x), "v"(b[i]));
+                else if constexpr (KIND == 12) asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
+                else asm volatile("v_sub_u32_e32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
             }
         b[0] ^= a[7];
     }
@@ -71,13 +81,22 @@ int main() {
     unsigned h[1024];
     for (int i = 0; i < 1024; i++) h[i] = rand();
     (void)hipMemcpy(din, h, 4096, hipMemcpyHostToDevice);
-    for (int w : {1, 2, 3, 4, 8}) {
+    const int ws[] = {2, 4, 8};
+    for (int w : ws) {
         run<0>("v_add", din, dout, dclk, w);
         run<1>("v_sad", din, dout, dclk, w);
         run<2>("v_xad", din, dout, dclk, w);
         run<3>("v_max3", din, dout, dclk, w);
         run<4>("add_sdwa", din, dout, dclk, w);
         run<5>("mad_u24", din, dout, dclk, w);
+        run<6>("add_e64", din, dout, dclk, w);
+        run<7>("sad_s", din, dout, dclk, w);
+        run<8>("xad_s", din, dout, dclk, w);
+        run<9>("max_e32", din, dout, dclk, w);
+        run<10>("mul_u24", din, dout, dclk, w);
+        run<11>("add3", din, dout, dclk, w);
+        run<12>("xor_e32", din, dout, dclk, w);
+        run<13>("sub_e32", din, dout, dclk, w);
     }
     return 0;
 }
