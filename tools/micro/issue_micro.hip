@@ -38,7 +38,18 @@ __global__ void __launch_bounds__(64) k(const unsigned *in, unsigned *out, unsig
                 else if constexpr (KIND == 10) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
                 else if constexpr (KIND == 11) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(x), "v"(b[i]));
                 else if constexpr (KIND == 12) asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
-                else asm volatile("v_sub_u32_e32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 13) asm volatile("v_sub_u32_e32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 14) asm volatile("v_lshrrev_b32_e32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 15) asm volatile("v_ashrrev_i32_e32 %0, 3, %0" : "+v"(a[i]));
+                else if constexpr (KIND == 16) asm volatile("v_ffbh_u32_e32 %0, %1" : "=v"(a[i]) : "v"(a[i] ^ x));
+                else if constexpr (KIND == 17) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 18) asm volatile("v_or_b32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 19) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(a[i]));
+                else if constexpr (KIND == 20) asm volatile("v_add_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a[i]));
+                else if constexpr (KIND == 21) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 22) asm volatile("v_lshl_or_b32 %0, %1, 3, %0" : "+v"(a[i]) : "v"(x));
+                else if constexpr (KIND == 23) asm volatile("v_cmp_gt_u32_e32 vcc, %0, %1" :: "v"(a[i]), "v"(x) : "vcc");
+                else asm volatile("v_min_i32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(x));
             }
         b[0] ^= a[7];
     }
@@ -81,7 +92,7 @@ int main() {
     unsigned h[1024];
     for (int i = 0; i < 1024; i++) h[i] = rand();
     (void)hipMemcpy(din, h, 4096, hipMemcpyHostToDevice);
-    const int ws[] = {2, 4, 8};
+    const int ws[] = {4, 8};
     for (int w : ws) {
         run<0>("v_add", din, dout, dclk, w);
         run<1>("v_sad", din, dout, dclk, w);
@@ -97,6 +108,17 @@ int main() {
         run<11>("add3", din, dout, dclk, w);
         run<12>("xor_e32", din, dout, dclk, w);
         run<13>("sub_e32", din, dout, dclk, w);
+        run<14>("lshr_e32", din, dout, dclk, w);
+        run<15>("ashr_imm", din, dout, dclk, w);
+        run<16>("ffbh", din, dout, dclk, w);
+        run<17>("cndmask", din, dout, dclk, w);
+        run<18>("or_e32", din, dout, dclk, w);
+        run<19>("bfe_u32", din, dout, dclk, w);
+        run<20>("add_dpp", din, dout, dclk, w);
+        run<21>("mul_lo", din, dout, dclk, w);
+        run<22>("lshl_or", din, dout, dclk, w);
+        run<23>("cmp_e32", din, dout, dclk, w);
+        run<24>("min_i32", din, dout, dclk, w);
     }
     return 0;
 }
