@@ -406,3 +406,39 @@ def test_streaminfo_replay_device_matches_host(n, shape, carried):
         enc.streaminfo_replay_device(d_fb.data_ptr(), n, mm.data_ptr())
         torch.cuda.synchronize()
         assert mm.cpu().tolist() == want
+
+
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_one_wave_analysis_matches_oracle(variant, monkeypatch):
+    """k_ana1 (fg_ana1.hpp: one wave per full 16-bit stereo frame, FLACGPU_ANA1=1 / 2) writes the
+    same frames and sizes as the restatement (and so as k_analyze), and the same decision records."""
+    monkeypatch.setenv("FLACGPU_ANA1", variant)
+    ch, bits, rate = 2, 16, 44100
+    lengths = [4096 * 9 + 17, 4096 * 3, 1, 4096 * 5 - 1, 4096 * 64]
+    fb = ch * bits // 8
+    offs, total = _layout(lengths, fb, [0, 4, 8, 12])
+    pcm_all = bytearray(total)
+    pcms = []
+    for s, n in enumerate(lengths):
+        pcm = synth.synth_pcm(n, ch, bits, rate, stream=40 + s)
+        pcm_all[offs[s]:offs[s] + len(pcm)] = pcm
+        pcms.append(pcm)
+    with _encoder(ch, bits, rate, max_frames=128) as enc:
+        res, _ = _run_plan(enc, bytes(pcm_all), offs, lengths, md5="join")
+    for s, n in enumerate(lengths):
+        ref, ref_sizes, ref_md5 = oracle_ref.encode_stream(pcms[s], ch, bits, rate)
+        got, sizes, md5 = res[s]
+        assert sizes == ref_sizes and got == ref and md5 == ref_md5, f"stream {s}"
+    # decision records of every candidate (66 frames incl. the special blocks) against the oracle's,
+    # from a fresh encoder (test_gpu_parity caches its encoders; this one must see FLACGPU_ANA1)
+    import test_gpu_parity as tp
+
+    saved = dict(tp._encoders)
+    tp._encoders.clear()
+    try:
+        tp._records_match(ch, bits, rate, 4096 * 66)
+    finally:
+        for e in tp._encoders.values():
+            e.close()
+        tp._encoders.clear()
+        tp._encoders.update(saved)

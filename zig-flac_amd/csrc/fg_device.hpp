@@ -1164,6 +1164,7 @@ __device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int3
 #endif
 
 #include "fg_fused.hpp"
+#include "fg_rice16.hpp"
 
 template <int B, int CLS, bool FULL, int MAXT, int NC, int LPW, bool FP = false>
 // FP  : fused single-pass encode (full 16-bit stereo frames only, fg_fused.hpp): the workgroup
@@ -1519,6 +1520,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // samples -- shared by the fixed predictor and (build-defined) the LPC orders.
         const uint32_t capp = bps > 16 ? 30u : 14u;
         const uint32_t maxp = capp < a.max_param ? capp : a.max_param;
+        // 16-bit fixed prediction on full frames: fg_rice16.hpp's search, whose parameter rows start
+        // at (1 << o) (PO = 0); every other path keeps (1 << o) - 1 (PO = 1)
+        constexpr bool P16 = FULL && CLS == 16 && LPW == 0 && !FP;
+        constexpr uint32_t PO = P16 ? 0u : 1u;
         uint64_t *psum = nullptr;
         uint32_t *pmax = nullptr;
         if constexpr (!FULL) {
@@ -1570,7 +1575,13 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                                uint8_t *pb, uint32_t &best_o, uint32_t &best_m) -> uint64_t {
             uint64_t tots[9];
             uint32_t fives[9];
-            if constexpr (FULL) {
+            if constexpr (P16) {
+                // 16-bit fixed prediction: power-of-two cost model, parameters at pb[(1 << o) + j]
+                // (fg_rice16.hpp)
+                const uint32_t S32[4] = {(uint32_t)S8[0], (uint32_t)S8[1], (uint32_t)S8[2], (uint32_t)S8[3]};
+                const uint32_t W8[4] = {bitlen32(O8[0]), bitlen32(O8[1]), bitlen32(O8[2]), bitlen32(O8[3])};
+                return rice_search16(S32, W8, kw, P, maxp, pb, l, best_o, best_m);
+            } else if constexpr (FULL) {
                 uint32_t W8[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) W8[q] = bitlen32(O8[q]);
@@ -1928,7 +1939,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 // residuals were not kept through the search (register pressure): reload the
                 // samples from the staged PCM and recompute them.
                 const uint32_t o = R.porder, param_len = 4u + R.method, w = R.waste;
-                const uint8_t *pp = par + cur * 512u + ((1u << o) - 1u);
+                const uint8_t *pp = par + cur * 512u + ((1u << o) - PO);
                 if (l == 0) {
                     const uint32_t p0 = pp[0];
                     seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
@@ -2025,7 +2036,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
 
         // ---- 11. the frame descriptor (fused: the written subframes' fields in LDS, see below)
         uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
-        const uint8_t *pp = par + cur * 512u + ((1u << R.porder) - 1u);
+        const uint8_t *pp = par + cur * 512u + ((1u << R.porder) - PO);
         if (FP && my_slot >= 0) {
             uint32_t *lbits = (uint32_t *)(smem + LY.lbits);
             lbits[64u * (uint32_t)my_slot + l] = seg;
