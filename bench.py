@@ -44,8 +44,10 @@ The JSON line also carries:
                    from HIP events on its stream, against 8 TB/s; `traffic` from the
                    committed rocprofv3 PMC summary of the same workload and kernel
                    (profiles/), else null; `limiter` = what DESIGN.md measures binds;
-  stream_curve  -- the same blocks per step at 8 .. 16384 concurrent streams: the
-                   per-stream MD5 chain is the Amdahl term (rank 0, N = 1);
+  stream_curve  -- the same blocks per step at 8 .. 65536 concurrent streams, each
+                   stream's MD5 on the engine the plan picks (host pool below the
+                   crossover, one GPU lane per stream above), verified; both
+                   engines timed near the crossover (rank 0, N = 1);
   end_to_end    -- BASELINE.md's host-buffer contract: 8 ten-minute WAV-sized PCM
                    buffers in host memory -> .flac files in host memory (H2D,
                    kernels, D2H, MD5 on host threads, 73-byte header) (rank 0, N = 1);
@@ -98,7 +100,7 @@ def parse():
     p.add_argument("--no-md5", action="store_true", help="skip the per-stream GPU MD5 (diagnostics only)")
     p.add_argument("--verify-streams", type=int, default=64, help="streams compared with the oracle after timing")
     p.add_argument("--no-curve", action="store_true")
-    p.add_argument("--curve", default="8,64,1024,8192,16384,32768,65536")
+    p.add_argument("--curve", default="8,64,256,1024,8192,16384,65536")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-files", default="8,16,32,64", help="file counts of the end-to-end curve")
     p.add_argument("--e2e-minutes", type=float, default=10.0)
@@ -158,7 +160,10 @@ def build_input(args, rank):
 # ---------------------------------------------------------------------------------------------
 # the GPU step loop (one plan = S streams x F blocks at fixed device offsets)
 class Workload:
-    def __init__(self, enc, d_pcm, S, F, fb, dev, md5=True):
+    """md5: True / "device" (carried per-stream state on the GPU, one lane per stream), "host"
+    (flacgpu_md5_plan_host on a host thread beside the encode, from the host copy h_pcm), False."""
+
+    def __init__(self, enc, d_pcm, S, F, fb, dev, md5=True, h_pcm=None):
         import flacgpu
         import numpy as np
         import torch
@@ -173,20 +178,36 @@ class Workload:
         self.d_fb = torch.empty(self.plan.n_frames, dtype=torch.int32, device=dev)
         self.d_off = torch.empty(self.plan.n_frames, dtype=torch.int64, device=dev)
         self.d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
-        self.d_state = torch.from_numpy(np.frombuffer(flacgpu.md5_states(S), dtype=np.uint8).copy()).to(dev)
-        self.md5 = md5
+        self.md5 = "device" if md5 is True else md5
+        if self.md5 == "host":
+            assert h_pcm is not None
+            self.h_pcm = h_pcm
+            self.h_state = (flacgpu.Md5State * S)()
+            flacgpu.load_library().flacgpu_md5_state_init(self.h_state, S)
+            self.d_state = None
+        else:
+            self.d_state = torch.from_numpy(np.frombuffer(flacgpu.md5_states(S), dtype=np.uint8).copy()).to(dev)
         self.stream = torch.cuda.Stream(dev)  # the encode's own stream (not the legacy null stream)
         self.md5_stream = torch.cuda.Stream(dev)  # in order: each stream's MD5 chain follows the last step's
         self.steps_done = 0
         torch.cuda.synchronize()  # the buffers above were filled on the default stream
 
     def step(self):
+        hasher = None
+        if self.md5 == "host":
+            # the segments' MD5 on the library's host pool, beside this step's GPU encode (ctypes
+            # releases the GIL for the call); the step ends when both have
+            hasher = threading.Thread(target=self.plan.md5_host,
+                                      args=(self.h_pcm.ctypes.data, self.h_state, None))
+            hasher.start()
         if self.steps_done:
             self.plan.advance(self.F, self.stream.cuda_stream)
         self.enc.encode_plan_device_ex(self.plan, self.d_pcm.data_ptr(), self.d_out.data_ptr(), self.out_cap,
                                        self.d_fb.data_ptr(), self.d_off.data_ptr(), self.d_tot.data_ptr(),
-                                       self.d_state.data_ptr() if self.md5 else None, None,
+                                       self.d_state.data_ptr() if self.md5 == "device" else None, None,
                                        stream=self.stream.cuda_stream, md5_stream=self.md5_stream.cuda_stream)
+        if hasher:
+            hasher.join()
         self.steps_done += 1
 
     def close(self):
@@ -216,8 +237,9 @@ def run_timed(w, steps, warmup, dist=None):
     return t1 - t0
 
 
-def verify(args, w, buf, fb, n_verify, dev):
-    """Last step's frames of a sample of streams == the oracle's; their carried MD5 == hashlib."""
+def verify(args, w, buf, fb, n_verify, dev, frames=True):
+    """Last step's frames of a sample of streams == the oracle's (frames=False: skipped); their
+    carried MD5 == hashlib."""
     import numpy as np
     import torch
 
@@ -234,7 +256,7 @@ def verify(args, w, buf, fb, n_verify, dev):
     first_number = (w.steps_done - 1) * w.F
     picks = sorted(set(int(x) for x in np.linspace(0, w.S - 1, min(n_verify, w.S))))
     n_per = w.F * 4096
-    for s in picks:
+    for s in picks if frames else []:
         f0 = w.plan.first_frame[s]
         f1 = w.plan.first_frame[s + 1] if s + 1 < w.S else int(w.plan.n_frames)
         a = int(offs[f0])
@@ -246,17 +268,22 @@ def verify(args, w, buf, fb, n_verify, dev):
         ok &= got == ref and [int(x) for x in sizes[f0:f1]] == ref_sizes
     md5_ok = None
     if w.md5:
-        # finalise every stream's carried state with an empty final segment, on the device
-        fin = enc.plan(w.offsets, [0] * w.S, final=[True] * w.S)
-        d_md5 = torch.zeros(16 * w.S, dtype=torch.uint8, device=dev)
-        d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
-        dummy = torch.zeros(16, dtype=torch.uint8, device=dev)
-        enc.encode_plan_device_ex(fin, w.d_pcm.data_ptr(), dummy.data_ptr(), 16, dummy.data_ptr(), dummy.data_ptr(),
-                                  d_tot.data_ptr(), w.d_state.data_ptr(), d_md5.data_ptr(),
-                                  stream=w.stream.cuda_stream)
-        enc.sync_check(w.stream.cuda_stream)
-        fin.close()
-        dig = d_md5.cpu().numpy().reshape(-1, 16)
+        if w.md5 == "host":
+            # finalise the carried host states with an empty final segment
+            dig = np.frombuffer(b"".join(flacgpu_md5_many([b""] * w.S, [True] * w.S, w.h_state)),
+                                dtype=np.uint8).reshape(-1, 16)
+        else:
+            # finalise every stream's carried state with an empty final segment, on the device
+            fin = enc.plan(w.offsets, [0] * w.S, final=[True] * w.S)
+            d_md5 = torch.zeros(16 * w.S, dtype=torch.uint8, device=dev)
+            d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
+            dummy = torch.zeros(16, dtype=torch.uint8, device=dev)
+            enc.encode_plan_device_ex(fin, w.d_pcm.data_ptr(), dummy.data_ptr(), 16, dummy.data_ptr(),
+                                      dummy.data_ptr(), d_tot.data_ptr(), w.d_state.data_ptr(), d_md5.data_ptr(),
+                                      stream=w.stream.cuda_stream)
+            enc.sync_check(w.stream.cuda_stream)
+            fin.close()
+            dig = d_md5.cpu().numpy().reshape(-1, 16)
         md5_ok = True
         for s in picks[:16]:
             pcm = bytes(buf[w.offsets[s]:w.offsets[s] + n_per * fb])
@@ -267,6 +294,12 @@ def verify(args, w, buf, fb, n_verify, dev):
         ok &= md5_ok
     return bool(ok), {"streams_compared": len(picks), "frame_numbers_from": first_number,
                       "md5_streams_compared": min(16, len(picks)) if w.md5 else 0}
+
+
+def flacgpu_md5_many(chunks, final, states):
+    import flacgpu
+
+    return flacgpu.md5_many(chunks, final, states)
 
 
 def kernel_times(enc):
@@ -400,23 +433,46 @@ def sharded_stream(args, rank, world, dist_mod, dev):
     return res
 
 
-def stream_curve(args, enc, d_pcm, fb, dev):
-    """Same blocks per step at S concurrent streams: encode vs the per-stream MD5 chain."""
+def stream_curve(args, enc, d_pcm, buf, fb, dev):
+    """Same blocks per step at S concurrent streams: the encode beside the per-stream MD5 chains,
+    on the engine the plan picks (flacgpu_plan_md5_engine: the host pool for a few long chains, one
+    GPU lane per stream above the crossover), MD5 verified at every point.  Near the crossover the
+    other engine is timed too (`other`), which is how DESIGN.md section 5c's crossover is measured."""
+    import flacgpu
+
     out = []
     for S in [int(x) for x in args.curve.split(",") if x]:
         if args.frames % S:
             continue
         F = args.frames // S
-        w = Workload(enc, d_pcm, S, F, fb, dev)
-        steps = 2 if F <= 64 else 1
-        dt = run_timed(w, steps, 1)
-        kt = kernel_times(enc)
-        per = {k: round(v[1] / v[0], 3) for k, v in kt.items() if v[0]}
-        samples = S * F * 4096 * steps
-        out.append({"streams": S, "blocks_per_stream_per_step": F, "value": round(samples / dt / 1e6, 1),
-                    "ms_per_step": round(dt / steps * 1e3, 3), "kernel_ms": per})
-        w.close()
+        probe = enc.plan([0] * S, [F * 4096] * S, final=[False] * S)
+        pick = "host" if probe.md5_engine() == flacgpu.MD5_HOST else "device"
+        probe.close()
+        engines = [pick] + ([{"host": "device", "device": "host"}[pick]] if 64 <= S <= 1024 else [])
+        point = {"streams": S, "blocks_per_stream_per_step": F, "md5_engine": pick}
+        for eng in engines:
+            w = Workload(enc, d_pcm, S, F, fb, dev, md5=eng, h_pcm=buf)
+            steps = 2 if F <= 64 else 1
+            dt = run_timed(w, steps, 1)
+            kt = kernel_times(enc)
+            ok, _ = verify(args, w, buf, fb, 2, dev, frames=False)
+            per = {k: round(v[1] / v[0], 3) for k, v in kt.items() if v[0]}
+            samples = S * F * 4096 * steps
+            res = {"value": round(samples / dt / 1e6, 1), "ms_per_step": round(dt / steps * 1e3, 3),
+                   "kernel_ms": per, "md5_ok": ok}
+            if eng == pick:
+                point.update(res)
+            else:
+                point["other"] = dict(engine=eng, **res)
+            w.close()
+        out.append(point)
     return out
+
+
+def _timed(fn):
+    t0 = time.perf_counter()
+    fn()
+    return time.perf_counter() - t0
 
 
 def end_to_end(args):
@@ -463,8 +519,14 @@ def end_to_end(args):
         rcs[i] = L.flacgpu_encode_file(encs[i].ctx, files[i].ctypes.data_as(ctypes.c_void_p), 2, n,
                                        outs[i].ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(lens[i]))
 
-    def run_all(nf):
-        th = [threading.Thread(target=one, args=(i,)) for i in range(nf)]
+    def frames_only(i):
+        # the same path without the MD5 and header: flacgpu_encode_frames (H2D, kernels, D2H)
+        n_out = ctypes.c_size_t(0)
+        rcs[i] = L.flacgpu_encode_frames(encs[i].ctx, files[i].ctypes.data_as(ctypes.c_void_p), 2, n, 0,
+                                         outs[i].ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n_out), None)
+
+    def run_all(nf, fn=one):
+        th = [threading.Thread(target=fn, args=(i,)) for i in range(nf)]
         t0 = time.perf_counter()
         for t in th:
             t.start()
@@ -476,8 +538,21 @@ def end_to_end(args):
     curve = []
     for nf in counts:
         best = min(run_all(nf) for _ in range(2))
+        # the host-MD5 bound at this file count: the same files' MD5 alone on the library's pool
+        # (flacgpu_md5_many: what the encode's hashing does, with no GPU work or other threads)
+        md5_alone = min(_timed(lambda: flacgpu.md5_many(files[:nf])) for _ in range(2))
+        ok_nf = all(r == 0 for r in rcs[:nf])
+        # ... and the GPU + PCIe path alone (frames only, no MD5): the other bound
+        frames_alone = min(run_all(nf, frames_only) for _ in range(2))
+        ok_nf &= all(r == 0 for r in rcs[:nf])
+        bound = max(md5_alone, frames_alone)
         curve.append({"files": nf, "value": round(nf * n / best / 1e6, 1), "wall_ms": round(best * 1e3, 2),
-                      "ok": all(r == 0 for r in rcs[:nf])})
+                      "md5_pool_alone_ms": round(md5_alone * 1e3, 2),
+                      "frames_alone_ms": round(frames_alone * 1e3, 2),
+                      "frac_of_md5_bound": round(md5_alone / best, 3),
+                      "frac_of_bound": round(bound / best, 3),
+                      "binding": "host_md5" if md5_alone >= frames_alone else "gpu_pcie_frames",
+                      "ok": ok_nf})
     ok = all(c["ok"] for c in curve)
     # bounds: one file's MD5 on one host core; pinned H2D bandwidth
     t0 = time.perf_counter()
@@ -936,7 +1011,7 @@ def main():
     curve = e2e = cpu = None
     if rank == 0 and world == 1:
         if not args.no_curve and not args.no_md5:
-            curve = stream_curve(args, enc, d_pcm, fb, dev)
+            curve = stream_curve(args, enc, d_pcm, buf, fb, dev)
         if not args.no_e2e and (args.config or "c2") == "c2":
             del d_pcm
             torch.cuda.empty_cache()

@@ -218,6 +218,28 @@ int flacgpu_encode_plan_device_ex(flacgpu_ctx *ctx, const flacgpu_plan *plan, co
                                   uint64_t *d_total, flacgpu_md5_state *d_md5_state, uint8_t *d_md5,
                                   void *hip_stream, void *md5_stream);
 
+/* The host engine of the same MD5 (md5.zig:3-31 over the bytes wav_reader.zig:66
+ * feeds it; finalised as Encoder.finalizeStreamInfoMd5, encoder.zig:168-170).
+ * flacgpu_md5_many advances n independent chains on the library's host hashing
+ * pool: chain i absorbs lens[i] bytes at data[i] from states[i] (host memory,
+ * the layout and `finished` rules of the device path above, so a stream's state
+ * may pass between the engines from one call to the next); final[i] != 0 (final
+ * NULL: every chain) pads the chain and writes its digest to digests[16 i] (if
+ * non-NULL).  states NULL: fresh chains, all final.  A chain that continues
+ * after the call must absorb whole 64-byte blocks.  Needs no GPU; blocks. */
+int flacgpu_md5_many(uint32_t n, const void *const *data, const uint64_t *lens, const uint8_t *final,
+                     flacgpu_md5_state *states, uint8_t *digests);
+/* flacgpu_md5_many over every segment of `plan`, read from h_pcm, a host copy
+ * of the device PCM buffer (same offsets), with the plan's final flags.  Run it
+ * on a host thread beside flacgpu_encode_plan_device_ex called with
+ * d_md5_state = d_md5 = NULL: few long streams then hash at host-core speed
+ * instead of one GPU lane each. */
+int flacgpu_md5_plan_host(const flacgpu_plan *plan, const void *h_pcm, flacgpu_md5_state *states, uint8_t *digests);
+/* The faster MD5 engine for this plan's segments: FLACGPU_MD5_HOST below the
+ * stream-count crossover (a few long chains), FLACGPU_MD5_DEVICE above it (the
+ * model and its measured constants: DESIGN.md section 5c). */
+int flacgpu_plan_md5_engine(const flacgpu_plan *plan);
+
 /* Synchronise hip_stream (NULL: the context's stream) and report the device-side
  * error word of the kernels queued so far (FLACGPU_ERR_OUTPUT_TOO_SMALL when a
  * frame would not fit out_cap, FLACGPU_ERR_INTERNAL on a violated invariant);

@@ -12,6 +12,7 @@ larger than the context (plan-owned descriptors), both MD5 schedules, streams
 spanning several calls with carried MD5 state, frame-number windows
 (flacgpu_plan_advance), and the device error word (flacgpu_sync_check).
 """
+import ctypes
 import hashlib
 
 import numpy as np
@@ -192,6 +193,57 @@ def test_streams_spanning_calls_carry_md5_state(ch, bits, rate):
         ref, ref_sizes, ref_md5 = oracle_ref.encode_stream(full[s], ch, bits, rate)
         assert sizes[s] == ref_sizes and outs[s] == ref, f"stream {s}"
         assert digest[s] == ref_md5 == hashlib.md5(full[s]).digest(), f"stream {s}: carried MD5"
+
+
+def test_host_md5_engine_matches_device_state_by_state():
+    """flacgpu_md5_plan_host (the plan path's host engine) carries the same per-stream state as the
+    device MD5, call by call, segments final and not, finished states left alone; and the engine
+    pick is the host pool for a few long streams, the GPU lanes for many short ones."""
+    torch, dev = _torch()
+    import flacgpu
+
+    ch, bits, rate = 2, 16, 44100
+    fb = ch * (bits // 8)
+    totals = [4096 * 5 + 77, 4096 * 3, 4096 * 4 + 4095, 4096]
+    seg = 2 * 4096
+    full = [synth.synth_pcm(n, ch, bits, rate, stream=700 + s) for s, n in enumerate(totals)]
+    pos = [0] * len(totals)
+    fnum = [0] * len(totals)
+    d_state = torch.from_numpy(np.frombuffer(flacgpu.md5_states(len(totals)), dtype=np.uint8).copy()).to(dev)
+    h_state = (flacgpu.Md5State * len(totals))()
+    flacgpu.load_library().flacgpu_md5_state_init(h_state, len(totals))
+    done = [False] * len(totals)
+    with _encoder(ch, bits, rate, max_frames=32) as enc:
+        for _ in range(4):
+            lens, fin = [], []
+            for s in range(len(totals)):
+                take = 0 if done[s] else min(totals[s] - pos[s], seg)
+                lens.append(take)
+                fin.append(done[s] or pos[s] + take == totals[s])
+            offs, size = _layout(lens, fb, (4, 0))
+            buf = bytearray(size)
+            for s in range(len(totals)):
+                buf[offs[s]:offs[s] + lens[s] * fb] = full[s][pos[s] * fb:(pos[s] + lens[s]) * fb]
+            res, d_state = _run_plan(enc, bytes(buf), offs, lens, md5="state", first_frames=fnum, final=fin,
+                                     states=d_state)
+            plan = enc.plan(offs, lens, first_frames=fnum, final=fin)
+            h_buf = np.frombuffer(bytes(buf), dtype=np.uint8)
+            dig = (ctypes.c_uint8 * (16 * len(totals)))()
+            plan.md5_host(h_buf.ctypes.data, h_state, ctypes.addressof(dig))
+            plan.close()
+            assert bytes(h_state) == d_state.cpu().numpy().tobytes(), "host and device MD5 states differ"
+            for s in range(len(totals)):
+                if fin[s]:
+                    assert bytes(dig)[16 * s:16 * s + 16] == res[s][2] == hashlib.md5(full[s]).digest()
+                pos[s] += lens[s]
+                fnum[s] += (lens[s] + 4095) // 4096
+                done[s] = fin[s]
+        assert all(done)
+        few = enc.plan([s * 4096 * 1024 * fb for s in range(8)], [4096 * 1024] * 8, final=[False] * 8)
+        many = enc.plan([s * 4096 * 16 * fb for s in range(16384)], [4096 * 16] * 16384, final=[False] * 16384)
+        assert few.md5_engine() == flacgpu.MD5_HOST and many.md5_engine() == flacgpu.MD5_DEVICE
+        few.close()
+        many.close()
 
 
 def test_non_final_segment_must_be_whole_frames():

@@ -1,0 +1,85 @@
+"""The plan path's host MD5 engine (flacgpu_md5_many, include/flacgpu.h) against hashlib: the
+digest the reference's Md5 wrapper (md5.zig:3-31) computes over the bytes wav_reader.zig:66
+feeds it, finalised as encoder.zig:168-170.  Host-only calls: these run without a GPU."""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "zig-flac_amd"))
+import flacgpu  # noqa: E402
+
+
+def _lib_or_skip():
+    try:
+        return flacgpu.load_library()
+    except OSError as e:  # pragma: no cover - the build check covers the library itself
+        pytest.skip(f"libflacgpu not built: {e}")
+
+
+def _chunks(n, rng, sizes):
+    return [rng.integers(0, 256, size=int(sizes[i]), dtype=np.uint8).tobytes() for i in range(n)]
+
+
+@pytest.mark.parametrize("n", [1, 3, 8, 40])
+def test_md5_many_fresh_matches_hashlib(n):
+    _lib_or_skip()
+    rng = np.random.default_rng(n)
+    # empty, sub-block, one block +- 1, and pool-sized (>= 4 KiB: hashed on the pool workers)
+    base = [0, 1, 55, 56, 63, 64, 65, 4095, 4096, 70000, 1 << 20]
+    sizes = [base[i % len(base)] + (i // len(base)) * 3 for i in range(n)]
+    chunks = _chunks(n, rng, sizes)
+    got = flacgpu.md5_many(chunks)
+    assert got == [hashlib.md5(c).digest() for c in chunks]
+
+
+def test_md5_many_carried_segments_and_finished_rule():
+    _lib_or_skip()
+    rng = np.random.default_rng(7)
+    n = 12
+    segs = [[rng.integers(0, 256, size=64 * int(rng.integers(0, 300)), dtype=np.uint8).tobytes()
+             for _ in range(3)] for _ in range(n)]
+    tails = [rng.integers(0, 256, size=int(rng.integers(0, 9000)), dtype=np.uint8).tobytes() for _ in range(n)]
+    states = (flacgpu.Md5State * n)()
+    flacgpu.load_library().flacgpu_md5_state_init(states, n)
+    for k in range(3):
+        got = flacgpu.md5_many([segs[s][k] for s in range(n)], final=[False] * n, states=states)
+        assert got == [None] * n
+        assert all(states[s].bytes == sum(len(x) for x in segs[s][:k + 1]) for s in range(n))
+    dig = flacgpu.md5_many(tails, final=[True] * n, states=states)
+    want = [hashlib.md5(b"".join(segs[s]) + tails[s]).digest() for s in range(n)]
+    assert dig == want
+    assert all(states[s].finished == 1 for s in range(n))
+    # finished: h is the digest (little-endian words), and later calls leave the state as it is
+    assert bytes(states[0].h) == want[0]
+    again = flacgpu.md5_many([b"x" * 64] * n, final=[True] * n, states=states)
+    assert again == want
+    flacgpu.md5_many([b"y" * 64] * n, final=[False] * n, states=states)
+    assert bytes(states[3].h) == want[3] and states[3].finished == 1
+
+
+def test_md5_many_rejects_partial_block_continuation():
+    _lib_or_skip()
+    states = (flacgpu.Md5State * 1)()
+    flacgpu.load_library().flacgpu_md5_state_init(states, 1)
+    with pytest.raises(flacgpu.FlacGpuError):
+        flacgpu.md5_many([b"z" * 100], final=[False], states=states)
+    with pytest.raises(flacgpu.FlacGpuError):
+        flacgpu.md5_many([b"z" * 128], final=[False], states=None)  # nowhere to carry the chain
+
+
+def test_md5_many_no_pool_matches(monkeypatch):
+    """FLACGPU_MD5_THREADS=-1 (each chain on the caller) gives the same digests: run in a child so
+    the pool's size is read afresh."""
+    _lib_or_skip()
+    import subprocess
+
+    code = ("import sys, hashlib; sys.path.insert(0, %r); import flacgpu;"
+            "c=[bytes([i]) * (5000 + 64 * i) for i in range(6)];"
+            "assert flacgpu.md5_many(c) == [hashlib.md5(x).digest() for x in c]; print('ok')"
+            % os.path.join(os.path.dirname(__file__), "..", "zig-flac_amd"))
+    env = dict(os.environ, FLACGPU_MD5_THREADS="-1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr

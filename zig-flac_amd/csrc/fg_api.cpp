@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -169,6 +170,10 @@ struct flacgpu_plan {
     uint64_t max_number = 0;       // largest frame number in the table (u36 check on advance)
     std::vector<uint64_t> first_frame;
     std::vector<uint32_t> full_slots;  // slot of each full job (host copy: ranges of the overlapped encode)
+    // host copies of the MD5 segments (the host engine, flacgpu_md5_plan_host)
+    std::vector<uint64_t> h_md5_offs, h_md5_lens;
+    std::vector<uint8_t> h_md5_fin;  // empty: all final
+    uint64_t md5_total = 0;          // bytes of all segments
     uint64_t out_bound = 0;
     uint8_t *d_desc = nullptr;  // per-plan descriptor area when larger than the context's
 };
@@ -1062,6 +1067,101 @@ void flacgpu_md5_state_init(flacgpu_md5_state *s, size_t n) {
     }
 }
 
+int flacgpu_md5_many(uint32_t n, const void *const *data, const uint64_t *lens, const uint8_t *final,
+                     flacgpu_md5_state *states, uint8_t *digests) {
+    if (n && (!data || !lens)) return FLACGPU_ERR_INVALID_INPUT;
+    for (uint32_t i = 0; i < n; i++) {
+        const bool fin = !final || final[i];
+        // the state carries no partial block: a chain continues only after whole 64-byte blocks
+        if (!fin && (!states || lens[i] % 64u)) return FLACGPU_ERR_INVALID_INPUT;
+        if (lens[i] && !data[i]) return FLACGPU_ERR_INVALID_INPUT;
+    }
+    std::vector<fg::HostMd5> hs;
+    std::vector<fg::HostMd5 *> hp;
+    std::vector<const uint8_t *> ps;
+    std::vector<size_t> ls;
+    std::vector<uint32_t> idx;
+    try {
+        hs.resize(n);
+        hp.reserve(n);
+        ps.reserve(n);
+        ls.reserve(n);
+        idx.reserve(n);
+    } catch (...) {
+        return FLACGPU_ERR_OUT_OF_MEMORY;
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        const bool fin = !final || final[i];
+        if (states && (states[i].finished & 1u)) {
+            // a finished chain stays as it is; a final segment reports its digest again
+            if (fin && digests)
+                for (int w = 0; w < 4; w++)
+                    for (int b = 0; b < 4; b++) digests[16 * i + 4 * w + b] = (uint8_t)(states[i].h[w] >> (8 * b));
+            continue;
+        }
+        if (states) {
+            std::memcpy(hs[i].h, states[i].h, 16);
+            hs[i].bytes = states[i].bytes;
+        }
+        hp.push_back(&hs[i]);
+        ps.push_back((const uint8_t *)data[i]);
+        ls.push_back((size_t)lens[i]);
+        idx.push_back(i);
+    }
+    fg::md5_pool_update_many(hp.data(), ps.data(), ls.data(), hp.size());
+    for (uint32_t i : idx) {
+        const bool fin = !final || final[i];
+        const uint64_t bytes = hs[i].bytes;
+        uint8_t dg[16];
+        if (fin) {
+            hs[i].final(dg);
+            if (digests) std::memcpy(digests + 16 * (size_t)i, dg, 16);
+        }
+        if (states) {
+            if (fin)
+                for (int w = 0; w < 4; w++)
+                    states[i].h[w] = (uint32_t)dg[4 * w] | (uint32_t)dg[4 * w + 1] << 8 | (uint32_t)dg[4 * w + 2] << 16 |
+                                     (uint32_t)dg[4 * w + 3] << 24;
+            else
+                std::memcpy(states[i].h, hs[i].h, 16);
+            states[i].bytes = bytes;
+            states[i].finished = fin ? 1u : 0u;
+            states[i].reserved = 0;
+        }
+    }
+    return FLACGPU_OK;
+}
+
+int flacgpu_md5_plan_host(const flacgpu_plan *p, const void *h_pcm, flacgpu_md5_state *states, uint8_t *digests) {
+    if (!p || (p->n_streams && !h_pcm)) return FLACGPU_ERR_INVALID_INPUT;
+    std::vector<const void *> ptrs;
+    try {
+        ptrs.resize(p->n_streams);
+    } catch (...) {
+        return FLACGPU_ERR_OUT_OF_MEMORY;
+    }
+    for (uint32_t s = 0; s < p->n_streams; s++) ptrs[s] = (const uint8_t *)h_pcm + p->h_md5_offs[s];
+    return flacgpu_md5_many(p->n_streams, ptrs.data(), p->h_md5_lens.data(),
+                            p->h_md5_fin.empty() ? nullptr : p->h_md5_fin.data(), states, digests);
+}
+
+int flacgpu_plan_md5_engine(const flacgpu_plan *p) {
+    if (!p || !p->n_streams) return FLACGPU_MD5_DEVICE;
+    // Time of each engine for the plan's segments, from the rates bench.py's stream_curve measured
+    // on MI355X: device -- one lane per stream at ~72 MB/s beside the encode,
+    // at most ~600 GB/s over the chip (16384 streams: 4.3 GB of MD5 in 7.1 ms); host -- the pool's
+    // workers at ~0.95 GB/s a chain, k chains interleaved on a worker (k <= 4) running k / g(k)
+    // times as long as one, g = 1, 1.7, 2.2, 2.6 (64 streams on 16 workers: 41 GB/s).
+    static const double g[5] = {1.0, 1.0, 1.7, 2.2, 2.6};
+    const double workers = std::max(1, fg::md5_pool_workers());
+    const double n = p->n_streams;
+    const double t_dev = std::max((double)p->md5_max_len / 72e6, (double)p->md5_total / 600e9);
+    const int k = (int)std::min(4.0, std::ceil(n / workers));
+    const double host_rate = 0.95e9 * std::min(n, workers) * g[k];
+    const double t_host = (double)p->md5_total / host_rate;
+    return t_host < t_dev ? FLACGPU_MD5_HOST : FLACGPU_MD5_DEVICE;
+}
+
 // ---- plans (device-resident batches of independent streams) --------------
 int flacgpu_plan_create_segments(flacgpu_ctx *c, uint32_t n_streams, const uint64_t *offs, const uint64_t *samples,
                                  uint32_t bytes_per_sample, const uint64_t *first_frame_numbers,
@@ -1099,6 +1199,7 @@ int flacgpu_plan_create_segments(flacgpu_ctx *c, uint32_t n_streams, const uint6
             p->first_frame[s] = slot;
             lens[s] = samples[s] * fbytes_in;
             p->md5_max_len = std::max(p->md5_max_len, lens[s]);
+            p->md5_total += lens[s];
             const uint64_t nf = frames_for(samples[s], bs);
             const uint64_t f0 = first_frame_numbers ? first_frame_numbers[s] : 0;
             for (uint64_t f = 0; f < nf; f++, slot++) {
@@ -1112,6 +1213,9 @@ int flacgpu_plan_create_segments(flacgpu_ctx *c, uint32_t n_streams, const uint6
             }
         }
         full.insert(full.end(), tail.begin(), tail.end());
+        p->h_md5_offs.assign(offs, offs + n_streams);
+        p->h_md5_lens = lens;
+        if (final_segment) p->h_md5_fin.assign(final_segment, final_segment + n_streams);
     } catch (...) {
         delete p;
         return FLACGPU_ERR_OUT_OF_MEMORY;

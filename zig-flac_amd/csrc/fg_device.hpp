@@ -1520,9 +1520,11 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // samples -- shared by the fixed predictor and (build-defined) the LPC orders.
         const uint32_t capp = bps > 16 ? 30u : 14u;
         const uint32_t maxp = capp < a.max_param ? capp : a.max_param;
-        // 16-bit fixed prediction on full frames: fg_rice16.hpp's search, whose parameter rows start
-        // at (1 << o) (PO = 0); every other path keeps (1 << o) - 1 (PO = 1)
-        constexpr bool P16 = FULL && CLS == 16 && LPW == 0 && !FP;
+        // P16: fg_rice16.hpp's power-of-two search for 16-bit fixed prediction on full frames
+        // (parameter rows at (1 << o), PO = 0).  Measured slower here (tools/ab.sh r4f: analysis
+        // 4.57 vs 4.45 ms per 262144 frames), so off: every path keeps the
+        // search below with rows at (1 << o) - 1 (PO = 1)
+        constexpr bool P16 = false && FULL && CLS == 16 && LPW == 0 && !FP;
         constexpr uint32_t PO = P16 ? 0u : 1u;
         uint64_t *psum = nullptr;
         uint32_t *pmax = nullptr;

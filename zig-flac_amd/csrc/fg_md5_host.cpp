@@ -144,6 +144,7 @@ struct Md5Job {
     const uint8_t *tail;
     size_t tail_len;
     bool done = false;
+    size_t *left = nullptr;  // a batch's count of unfinished jobs (run_many)
 };
 
 class Md5Pool {
@@ -184,6 +185,60 @@ class Md5Pool {
         }
         h->update(job.tail, job.tail_len);
     }
+    // n updates at once (independent chains): the long ones are queued together, so the workers
+    // interleave up to four of them per core; the short ones are hashed on the caller meanwhile
+    void run_many(HostMd5 *const *hs, const uint8_t *const *ps, const size_t *lens, size_t n) {
+        if (workers_ == 0 || getpid() != owner_) {
+            for (size_t i = 0; i < n; i++) hs[i]->update(ps[i], lens[i]);
+            return;
+        }
+        struct Part {
+            HostMd5 *h;
+            const uint8_t *p;
+            size_t len;
+        };
+        std::vector<Md5Job> jobs;
+        std::vector<Part> own;
+        jobs.reserve(n);  // the queue holds pointers into it
+        size_t left = 0;
+        for (size_t i = 0; i < n; i++) {
+            HostMd5 *h = hs[i];
+            const uint8_t *p = ps[i];
+            size_t len = lens[i];
+            if (h->fill && len) {
+                const size_t take = len < 64u - h->fill ? len : 64u - h->fill;
+                h->update(p, take);
+                p += take;
+                len -= take;
+            }
+            if (h->fill || len < 64u * 64u) {
+                own.push_back({h, p, len});
+                continue;
+            }
+            Md5Job j;
+            j.h = h;
+            j.p = p;
+            j.nb = len / 64u;
+            j.tail = p + j.nb * 64u;
+            j.tail_len = len - j.nb * 64u;
+            j.left = &left;
+            h->bytes += j.nb * 64u;
+            jobs.push_back(j);
+        }
+        if (!jobs.empty()) {
+            std::lock_guard<std::mutex> lk(m_);
+            left = jobs.size();
+            for (auto &j : jobs) q_.push_back(&j);
+            cv_.notify_all();
+        }
+        for (auto &o : own) o.h->update(o.p, o.len);
+        if (!jobs.empty()) {
+            std::unique_lock<std::mutex> lk(m_);
+            done_cv_.wait(lk, [&] { return left == 0; });
+        }
+        for (auto &j : jobs) j.h->update(j.tail, j.tail_len);
+    }
+    int workers() const { return workers_; }
 
   private:
     static constexpr int kMaxChains = 4;
@@ -226,16 +281,21 @@ class Md5Pool {
         for (;;) {
             {
                 // an idle worker takes one message; a busy one adds more only while no worker is
-                // idle (so a few files spread over the workers, many files share them)
+                // idle (so a few files spread over the workers, many files share them), and only
+                // up to its even share of the chains in flight (so 32 files on 16 workers run two
+                // chains each rather than four on a few workers and one on the rest)
                 std::unique_lock<std::mutex> lk(m_);
                 if (act.empty()) {
                     idle_++;
                     cv_.wait(lk, [&] { return !q_.empty(); });
                     idle_--;
                 }
-                while ((int)act.size() < kMaxChains && !q_.empty() && (act.empty() || idle_ == 0)) {
+                const size_t chains = active_ + q_.size();
+                const size_t share = std::max<size_t>(1, std::min<size_t>(kMaxChains, (chains + workers_ - 1) / workers_));
+                while (act.size() < share && !q_.empty() && (act.empty() || idle_ == 0)) {
                     act.push_back(q_.front());
                     q_.pop_front();
+                    active_++;
                 }
             }
             size_t nb = kChunk;
@@ -261,7 +321,11 @@ class Md5Pool {
             if (finished) {
                 std::lock_guard<std::mutex> lk(m_);
                 for (auto *j : act)
-                    if (j->nb == 0) j->done = true;
+                    if (j->nb == 0) {
+                        j->done = true;
+                        active_--;
+                        if (j->left) --*j->left;
+                    }
                 done_cv_.notify_all();
                 act.erase(std::remove_if(act.begin(), act.end(), [](Md5Job *j) { return j->done; }), act.end());
             }
@@ -271,12 +335,19 @@ class Md5Pool {
     std::condition_variable cv_, done_cv_;
     std::deque<Md5Job *> q_;
     int workers_ = 0, idle_ = 0;
+    size_t active_ = 0;  // chains held by the workers
     const pid_t owner_;  // the process whose workers these are
 };
 
 }  // namespace
 
 void md5_pool_update(HostMd5 *h, const void *data, size_t len) { Md5Pool::get().run(h, (const uint8_t *)data, len); }
+
+void md5_pool_update_many(HostMd5 *const *hs, const uint8_t *const *data, const size_t *lens, size_t n) {
+    Md5Pool::get().run_many(hs, data, lens, n);
+}
+
+int md5_pool_workers() { return Md5Pool::get().workers(); }
 
 void HostMd5::reset() {
     h[0] = 0x67452301u;

@@ -24,8 +24,15 @@ struct HostMd5 {
 // update runs on a pool worker that hashes up to four callers' messages at once, their chains
 // interleaved step by step (one MD5 chain leaves most of a core's ALU ports idle), so files
 // encoded concurrently hash 2-3x faster per core than one scalar chain each.  Blocks until done.
-// FLACGPU_MD5_THREADS sets the worker count (default: OMP_NUM_THREADS, else the affinity mask's
-// CPUs; -1: no pool, each caller hashes its own chain).
+// FLACGPU_MD5_THREADS sets the worker count (default: the process's CPU share -- the cgroup quota,
+// else the affinity mask's CPUs; -1: no pool, each caller hashes its own chain).
 void md5_pool_update(HostMd5 *h, const void *data, size_t len);
+
+// hs[i]->update(data[i], lens[i]) for n independent chains on the pool, queued together (the
+// plan path's host engine: every stream segment of a batch at once).  Blocks until all are done.
+void md5_pool_update_many(HostMd5 *const *hs, const uint8_t *const *data, const size_t *lens, size_t n);
+
+// the pool's worker count (0: every caller hashes its own chain)
+int md5_pool_workers();
 
 }  // namespace fg

@@ -101,6 +101,23 @@ def md5_states(n: int) -> bytes:
     return bytes(arr)[: 32 * n]
 
 
+def md5_many(chunks: Sequence, final: Optional[Sequence[bool]] = None, states=None) -> list:
+    """flacgpu_md5_many: advance len(chunks) independent MD5 chains on the library's host pool
+    (md5.zig:3-31).  `states` (an (Md5State * n) array, or None for fresh chains) is updated in
+    place; returns the digests (16 bytes each; None for a chain that is not final)."""
+    import numpy as np
+
+    n = len(chunks)
+    views = [np.frombuffer(c, dtype=np.uint8) if len(c) else np.zeros(1, np.uint8) for c in chunks]
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[v.ctypes.data for v in views])
+    lens = (ctypes.c_uint64 * max(n, 1))(*[len(c) for c in chunks])
+    fin = (ctypes.c_uint8 * max(n, 1))(*[1 if f else 0 for f in final]) if final is not None else None
+    dig = (ctypes.c_uint8 * max(16 * n, 1))()
+    _check(load_library().flacgpu_md5_many(n, ptrs, lens, fin, states, dig), "md5_many")
+    raw = bytes(dig)
+    return [raw[16 * i:16 * i + 16] if final is None or final[i] else None for i in range(n)]
+
+
 class WavInfo(ctypes.Structure):
     """flacgpu_wav_info: WavReader's view of a WAV header (wav_reader.zig:116-170)."""
     _fields_ = [("sample_rate", ctypes.c_uint32), ("channels", ctypes.c_uint16), ("bits_per_sample", ctypes.c_uint16),
@@ -203,6 +220,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_md5_set_engine": (I32, [P, I32]),
         "flacgpu_md5_get_engine": (I32, [P]),
         "flacgpu_md5_state_init": (None, [P, SZ]),
+        "flacgpu_md5_many": (I32, [U32, P, P, P, P, P]),
+        "flacgpu_md5_plan_host": (I32, [P, P, P, P]),
+        "flacgpu_plan_md5_engine": (I32, [P]),
         "flacgpu_plan_destroy": (None, [P]),
         "flacgpu_plan_frames": (U64, [P]),
         "flacgpu_plan_out_bound": (U64, [P]),
@@ -228,7 +248,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_close_multi": (None, [P]),
         "flacgpu_multi_encode_frames": (I32, [P, P, U32, U64, U64, P, SZ, ctypes.POINTER(SZ), P]),
     }
+    # an older build named by FLACGPU_LIB (same-box A/B runs, tools/ab.sh) may predate later entry
+    # points: those stay unbound there; the in-tree library must export every one
+    other_build = path != os.path.join(HERE, "build", "libflacgpu.so")
     for name, (res, args) in sig.items():
+        if other_build and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -246,6 +271,7 @@ def exported_symbols() -> list:
         "flacgpu_plan_create_segments", "flacgpu_plan_advance", "flacgpu_encode_plan_device_ex", "flacgpu_sync_check",
         "flacgpu_streaminfo_replay_device",
         "flacgpu_md5_set_engine", "flacgpu_md5_get_engine", "flacgpu_md5_state_init",
+        "flacgpu_md5_many", "flacgpu_md5_plan_host", "flacgpu_plan_md5_engine",
         "flacgpu_set_timing",
         "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_set_overlap", "flacgpu_get_records",
         "flacgpu_get_config", "flacgpu_wav_parse", "flacgpu_streaminfo_init", "flacgpu_streaminfo_update_frame_size",
@@ -294,6 +320,15 @@ class Plan:
     def advance(self, frames: int, stream: Optional[int] = None) -> None:
         """flacgpu_plan_advance: the next window of the same streams (frame numbers + frames)."""
         _check(self.enc.lib.flacgpu_plan_advance(self.handle, frames, _stream(stream)), "plan_advance")
+
+    def md5_engine(self) -> int:
+        """flacgpu_plan_md5_engine: MD5_HOST below the stream-count crossover, else MD5_DEVICE."""
+        return self.enc.lib.flacgpu_plan_md5_engine(self.handle)
+
+    def md5_host(self, h_pcm: int, states=None, digests: Optional[int] = None) -> None:
+        """flacgpu_md5_plan_host: every segment's MD5 on the host pool from the host copy h_pcm
+        (address; same offsets as the device buffer), states/digests in host memory."""
+        _check(self.enc.lib.flacgpu_md5_plan_host(self.handle, h_pcm, states, digests), "md5_plan_host")
 
     def close(self) -> None:
         if self.handle:
