@@ -306,6 +306,14 @@ size_t flacgpu_vorbis_comment_bytes(int last_metadata, uint8_t out[31]);
  * that runs beside the GPU encode). */
 int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
                         uint8_t *out, size_t out_cap, size_t *out_len);
+/* flacgpu_encode_file for n_files PCM buffers at once on one context: out[i]
+ * (capacity out_cap[i]) receives exactly the bytes flacgpu_encode_file writes for
+ * file i, out_len[i] their count (all 0 on an error).  Every file's frames go
+ * through one pipelined upload / encode / download schedule that runs on from
+ * file to file, and every file's MD5 is hashed on the host pool in one batch
+ * beside it: the many-files-per-GPU form of wav2flac.zig:10-97. */
+int flacgpu_encode_files(flacgpu_ctx *ctx, uint32_t n_files, const void *const *pcm, uint32_t bytes_per_sample,
+                         const uint64_t *n_samples, uint8_t *const *out, const size_t *out_cap, size_t *out_len);
 /* The whole conversion of an in-memory WAV file on HIP device `device`
  * (Config.default for the WAV's channels and bit depth). */
 int flacgpu_wav_to_flac(int device, const void *wav, size_t wav_len, uint8_t *out, size_t out_cap, size_t *out_len);

@@ -118,6 +118,26 @@ def test_gpu_encode_file_matches_oracle(ch, bits, rate, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (2, 24, 96000), (8, 24, 96000)])
+@pytest.mark.parametrize("engine", ["host", "device"])
+def test_gpu_encode_files_matches_oracle(ch, bits, rate, engine):
+    """flacgpu_encode_files: each file byte-identical to the oracle's whole-file encode; the
+    pipeline runs on across files (max_frames=8: 4-frame chunks, so files end mid-pipeline and
+    chunks never span two files), empty and sub-frame files included."""
+    lens = [3 * 4096 + 1000, 1, 0, 9 * 4096, 4096 + 5, 17 * 4096 + 4095, 7]
+    pcms = [synth.synth_pcm(n, ch, bits, rate, stream=40 + i) if n else b"" for i, n in enumerate(lens)]
+    with flacgpu.Encoder(ch, bits, rate, max_frames=8) as enc:
+        if engine == "device":
+            enc.set_md5_engine(flacgpu.MD5_DEVICE)
+        outs = enc.encode_files(pcms)
+        again = enc.encode_files(pcms[::-1])
+    for i, pcm in enumerate(pcms):
+        ref = oracle_ref.encode_file(pcm, ch, bits, rate)
+        assert outs[i] == ref, f"file {i}"
+        assert again[len(pcms) - 1 - i] == ref, f"file {i} (reversed batch)"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("block", [1152, 4096, 192, 4000])
 def test_gpu_encode_file_block_sizes(block):
     """STREAMINFO min/max block size follows the context's block size (the reference only

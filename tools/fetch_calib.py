@@ -25,9 +25,9 @@ def main():
                 fetch[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     rows = []
     for r in runs:
-        key = next((k for k in fetch if k.startswith(r["kernel"] + "(") or k.startswith(r["kernel"])), None)
+        key = next((k for k in fetch if r["kernel"] + "(" in k), None)
         fs = sum(fetch[key]) / len(fetch[key]) * 1024 if key else None
-        ns = next((v for k, v in stats.items() if k.startswith(r["kernel"])), None)
+        ns = next((v for k, v in stats.items() if r["kernel"] + "(" in k), None)
         rows.append(dict(r, fetch_bytes=fs, fetch_over_bytes=round(fs / r["bytes"], 4) if fs else None,
                          trace_avg_ms=round(ns / 1e6, 4) if ns else None))
     out = {"tag": tag, "note": "fetch_over_bytes = FETCH_SIZE KiB x 1024 / bytes the kernel reads (no x2 applied)",

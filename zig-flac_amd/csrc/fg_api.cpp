@@ -90,6 +90,10 @@ struct flacgpu_ctx {
     hipStream_t stream = nullptr, aux = nullptr;
     hipStream_t dl = nullptr;  // download stream of the pipelined host-buffer path
     hipEvent_t fork = nullptr, join = nullptr;
+    // host waits of the pipelined host-buffer path (two chunk sets, the download stream, the end):
+    // blocking-sync events, so a waiting thread sleeps instead of spinning on a core the MD5 pool
+    // and the other files' threads need (FLACGPU_SPIN_SYNC=1: spinning events, A/B)
+    hipEvent_t hw[4] = {nullptr, nullptr, nullptr, nullptr};
     uint16_t *d_crc_pow = nullptr, *d_crc_join = nullptr, *d_crc_pow4 = nullptr;
     // full 16-bit two-channel frames are packed by k_pack4 (four waves per subframe): 512 threads
     uint32_t nt_pack4 = 0, lds_pack4 = 0, crc_hmax4 = 0;
@@ -133,6 +137,7 @@ struct flacgpu_ctx {
     // ovl_ana / ovl_pack workgroups per CU so both are resident on every CU
     uint32_t ovl_chunks = 0, ovl_ana = 2, ovl_pack = 2, ovl_min_frames = 4096;
     bool xcd_queue = true;  // split analysis: per-XCD item queues (fg_device.hpp xcd_ticket)
+    bool pack_xcdq = true;  // split pack: the same (fg_packw.hpp)
     // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp): analysis and pack in
     // one kernel, frame offsets by an in-kernel look-back over per-slot status words
     bool fused = false;
@@ -347,6 +352,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
             h.image_bytes = c->image_split;
             h.crc_pow4 = c->d_crc_pows;
             h.crc_hmax4 = c->crc_hmaxs;
+            h.xcd_queue = c->pack_xcdq ? 1u : 0u;
             HIPCHK(launch_stage(1, h, true, c->nt_psplit, c->lds_psplit, s));
         } else if (c->nt_pack4) {
             HIPCHK(launch_stage(1, h, true, c->nt_pack4, c->lds_pack4, s));
@@ -476,6 +482,25 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
 int check_device_error(flacgpu_ctx *c) {
     uint32_t err = 0;
     HIPCHK(hipMemcpy(&err, c->d_err, 4, hipMemcpyDeviceToHost));
+    if (err) {
+        hipMemset(c->d_err, 0, 4);
+        return (err & 2u) && !(err & 1u) ? FLACGPU_ERR_OUTPUT_TOO_SMALL : FLACGPU_ERR_INTERNAL;
+    }
+    return FLACGPU_OK;
+}
+
+// Wait on the host for everything queued on st so far, through the context's event i (blocking
+// sync: the thread sleeps).
+hipError_t wait_host(flacgpu_ctx *c, hipStream_t st, int i) {
+    hipError_t e = hipEventRecord(c->hw[i], st);
+    return e != hipSuccess ? e : hipEventSynchronize(c->hw[i]);
+}
+
+// check_device_error after a blocking wait on st (the pipelined path's end)
+int check_device_error_on(flacgpu_ctx *c, hipStream_t st) {
+    uint32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&err, c->d_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(wait_host(c, st, 3));
     if (err) {
         hipMemset(c->d_err, 0, 4);
         return (err & 2u) && !(err & 1u) ? FLACGPU_ERR_OUTPUT_TOO_SMALL : FLACGPU_ERR_INTERNAL;
@@ -637,6 +662,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     // overlapped encode: ranges per call, workgroups per CU of the analysis / pack grids (A/B knobs)
     if (const char *e = std::getenv("FLACGPU_OVERLAP")) c->ovl_chunks = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_XCD_QUEUE")) c->xcd_queue = e[0] != '0';  // A/B knob
+    if (const char *e = std::getenv("FLACGPU_PACK_XCDQ")) c->pack_xcdq = e[0] != '0';   // A/B knob
     if (const char *e = std::getenv("FLACGPU_OVL_ANA")) c->ovl_ana = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_OVL_PACK")) c->ovl_pack = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_OVL_MIN")) c->ovl_min_frames = (uint32_t)std::max(1, std::atoi(e));
@@ -712,6 +738,12 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (hipStreamCreateWithFlags(&c->ovl, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    {
+        const char *e = std::getenv("FLACGPU_SPIN_SYNC");
+        const unsigned fl = hipEventDisableTiming | ((e && e[0] == '1') ? 0u : hipEventBlockingSync);
+        for (hipEvent_t &ev : c->hw)
+            if (hipEventCreateWithFlags(&ev, fl) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    }
 
     // CRC-16 shift constants of the table-free fold (mod Q, fg_device.hpp crc_lane_q): thread t
     // of T folds 2H words, followed by 2H (T - 1 - t) words and the CRC's z^16
@@ -795,6 +827,8 @@ void flacgpu_close(flacgpu_ctx *c) {
     hipFree(c->d_md5_blocks);
     if (c->fork) hipEventDestroy(c->fork);
     if (c->join) hipEventDestroy(c->join);
+    for (hipEvent_t e : c->hw)
+        if (e) hipEventDestroy(e);
     if (c->aux) hipStreamDestroy(c->aux);
     if (c->dl) hipStreamDestroy(c->dl);
     if (c->ovl) hipStreamDestroy(c->ovl);
@@ -806,24 +840,30 @@ void flacgpu_close(flacgpu_ctx *c) {
 // device buffers split into two halves, chunk i+1 is uploaded and encoded on c->stream
 // while a worker thread downloads chunk i's frames on c->dl (pageable copies block the
 // issuing thread, so the two directions need two threads).  Output bytes and frame sizes
-// are identical to the sequential loop; only the schedule differs.
-static int encode_frames_pipelined(flacgpu_ctx *c, const uint8_t *src, uint64_t n_samples, uint64_t first_frame_number,
-                                   uint8_t *out, size_t out_cap, size_t *out_len, uint32_t *frame_bytes) {
+// are identical to the sequential loop; only the schedule differs.  The input is a list of
+// segments (files, flacgpu_encode_files): chunks never span two, and the pipeline runs on
+// from one segment into the next instead of draining at each file's end.
+struct PipeSeg {
+    const uint8_t *src;
+    uint64_t n_samples, first_frame_number;
+    uint8_t *out;
+    size_t out_cap, written;
+    uint32_t *frame_bytes;  // may be NULL
+};
+
+static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     const uint32_t bs = c->cfg.block_size;
     const uint64_t stride = (uint64_t)bs * c->C * c->B;
-    const uint64_t total_frames = frames_for(n_samples, bs);
     // chunks of at most 2048 frames (32 MiB of 16-bit stereo) so that long inputs keep both
     // PCIe directions busy; the halves of the context's buffers hold one chunk each
     const uint64_t F = std::min<uint64_t>(c->max_frames / 2u, 2048u);
     const uint64_t pcm_half = (uint64_t)(c->max_frames / 2u) * kBlock * c->C * c->B;  // 16-B multiple
     const uint64_t out_half = (uint64_t)(c->max_frames / 2u) * c->image_bytes;
     const uint64_t fb_half = c->max_frames / 2u;
-    hipEvent_t done[2] = {get_event(c), get_event(c)};
-    if (!done[0] || !done[1]) return FLACGPU_ERR_DEVICE;
-    size_t written = 0;
+    hipEvent_t *done = c->hw;  // chunk sets 0 and 1 (blocking-sync events)
     int wrc = FLACGPU_OK;  // the worker's result
     std::thread worker;
-    auto download = [&](int set, uint64_t frame0, uint64_t nf) {
+    auto download = [&](int set, PipeSeg *sg, uint64_t frame0, uint64_t nf) {
         wrc = FLACGPU_OK;
         if (hipSetDevice(c->device) != hipSuccess || hipEventSynchronize(done[set]) != hipSuccess) {
             wrc = FLACGPU_ERR_DEVICE;
@@ -831,75 +871,104 @@ static int encode_frames_pipelined(flacgpu_ctx *c, const uint8_t *src, uint64_t 
         }
         uint64_t total = 0;
         if (hipMemcpyAsync(&total, c->d_total + set, 8, hipMemcpyDeviceToHost, c->dl) != hipSuccess ||
-            hipStreamSynchronize(c->dl) != hipSuccess) {
+            wait_host(c, c->dl, 2) != hipSuccess) {
             wrc = FLACGPU_ERR_DEVICE;
             return;
         }
-        if (written + total > out_cap) {
+        if (sg->written + total > sg->out_cap) {
             wrc = FLACGPU_ERR_OUTPUT_TOO_SMALL;
             return;
         }
-        if ((frame_bytes && hipMemcpyAsync(frame_bytes + frame0, c->d_fbytes + set * fb_half, nf * 4, hipMemcpyDeviceToHost,
-                                           c->dl) != hipSuccess) ||
-            hipMemcpyAsync(out + written, c->d_out + set * out_half, total, hipMemcpyDeviceToHost, c->dl) != hipSuccess ||
-            hipStreamSynchronize(c->dl) != hipSuccess) {
+        if ((sg->frame_bytes && hipMemcpyAsync(sg->frame_bytes + frame0, c->d_fbytes + set * fb_half, nf * 4,
+                                               hipMemcpyDeviceToHost, c->dl) != hipSuccess) ||
+            hipMemcpyAsync(sg->out + sg->written, c->d_out + set * out_half, total, hipMemcpyDeviceToHost, c->dl) !=
+                hipSuccess ||
+            wait_host(c, c->dl, 2) != hipSuccess) {
             wrc = FLACGPU_ERR_DEVICE;
             return;
         }
-        written += total;
+        sg->written += total;
     };
     int rc = FLACGPU_OK;
-    uint64_t frame0 = 0;
-    for (int set = 0; frame0 < total_frames && rc == FLACGPU_OK; set ^= 1) {
-        const uint64_t nf = std::min<uint64_t>(F, total_frames - frame0);
-        const uint64_t s0 = frame0 * bs;
-        const uint64_t ns = std::min<uint64_t>(nf * bs, n_samples - s0);
-        uint8_t *dp = c->d_pcm + set * pcm_half;
-        // chunk i - 1's download (worker) overlaps this upload; chunk i - 2 used this half
-        if (hipMemcpyAsync(dp, src + s0 * c->C * c->B, ns * c->C * c->B, hipMemcpyHostToDevice, c->stream) !=
-            hipSuccess) {
-            rc = FLACGPU_ERR_DEVICE;
-            break;
+    int set = 0;
+    for (size_t si = 0; si < nseg && rc == FLACGPU_OK; si++) {
+        PipeSeg *sg = &segs[si];
+        sg->written = 0;
+        const uint64_t total_frames = frames_for(sg->n_samples, bs);
+        for (uint64_t frame0 = 0; frame0 < total_frames && rc == FLACGPU_OK; set ^= 1) {
+            const uint64_t nf = std::min<uint64_t>(F, total_frames - frame0);
+            const uint64_t s0 = frame0 * bs;
+            const uint64_t ns = std::min<uint64_t>(nf * bs, sg->n_samples - s0);
+            uint8_t *dp = c->d_pcm + set * pcm_half;
+            // chunk i - 1's download (worker) overlaps this upload; chunk i - 2 used this half
+            if (hipMemcpyAsync(dp, sg->src + s0 * c->C * c->B, ns * c->C * c->B, hipMemcpyHostToDevice, c->stream) !=
+                hipSuccess) {
+                rc = FLACGPU_ERR_DEVICE;
+                break;
+            }
+            if (launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, sg->first_frame_number + frame0, (uint32_t)nf,
+                                 c->stream) != hipSuccess) {
+                rc = FLACGPU_ERR_DEVICE;
+                break;
+            }
+            const uint64_t n_full = (bs == (uint32_t)kBlock) ? ns / kBlock : 0;
+            if ((rc = encode_core(c, dp, c->d_jobs, n_full, nf - n_full, c->d_desc, c->d_fbytes + set * fb_half,
+                                  c->d_out + set * out_half, out_half, c->d_offsets, c->d_total + set, c->stream)))
+                break;
+            if (hipEventRecord(done[set], c->stream) != hipSuccess) {
+                rc = FLACGPU_ERR_DEVICE;
+                break;
+            }
+            // chunk i - 1's download ran beside this chunk's upload and encode (the other half);
+            // it must end before the next worker (output order) and before half set ^ 1 is reused
+            if (worker.joinable()) {
+                worker.join();
+                if ((rc = wrc)) break;
+            }
+            try {
+                worker = std::thread(download, set, sg, frame0, nf);
+            } catch (const std::system_error &) {
+                download(set, sg, frame0, nf);  // no thread to be had: download in line
+                if ((rc = wrc)) break;
+            }
+            frame0 += nf;
         }
-        if (launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, first_frame_number + frame0, (uint32_t)nf,
-                             c->stream) != hipSuccess) {
-            rc = FLACGPU_ERR_DEVICE;
-            break;
-        }
-        const uint64_t n_full = (bs == (uint32_t)kBlock) ? ns / kBlock : 0;
-        if ((rc = encode_core(c, dp, c->d_jobs, n_full, nf - n_full, c->d_desc, c->d_fbytes + set * fb_half,
-                              c->d_out + set * out_half, out_half, c->d_offsets, c->d_total + set, c->stream)))
-            break;
-        if (hipEventRecord(done[set], c->stream) != hipSuccess) {
-            rc = FLACGPU_ERR_DEVICE;
-            break;
-        }
-        // chunk i - 1's download ran beside this chunk's upload and encode (the other half);
-        // it must end before the next worker (output order) and before half set ^ 1 is reused
-        if (worker.joinable()) {
-            worker.join();
-            if ((rc = wrc)) break;
-        }
-        try {
-            worker = std::thread(download, set, frame0, nf);
-        } catch (const std::system_error &) {
-            download(set, frame0, nf);  // no thread to be had: download in line
-            if ((rc = wrc)) break;
-        }
-        frame0 += nf;
     }
     if (worker.joinable()) {
         worker.join();
         if (rc == FLACGPU_OK) rc = wrc;
     }
-    hipStreamSynchronize(c->stream);
-    c->event_pool.push_back(done[0]);
-    c->event_pool.push_back(done[1]);
-    if (rc) return rc;
-    if ((rc = check_device_error(c))) return rc;
-    *out_len = written;
-    return FLACGPU_OK;
+    if (rc) {
+        hipStreamSynchronize(c->stream);
+        return rc;
+    }
+    return check_device_error_on(c, c->stream);
 }
+
+}  // extern "C"
+
+int fg::ctx_encode_segments(flacgpu_ctx *c, uint32_t n, const uint8_t *const *src, const uint64_t *n_samples,
+                            uint8_t *const *out, const size_t *out_cap, size_t *out_len, uint32_t *const *frame_bytes) {
+    if (c->max_frames < 2 || c->records_on) return FLACGPU_ERR_INVALID_CONFIG;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<PipeSeg> segs;
+    try {
+        segs.resize(n);
+    } catch (...) {
+        return FLACGPU_ERR_OUT_OF_MEMORY;
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t nf = frames_for(n_samples[i], c->cfg.block_size);
+        if (nf && nf - 1 > (1ull << 36) - 1) return FLACGPU_ERR_INVALID_INPUT;  // u36 frame numbers
+        segs[i] = PipeSeg{src[i], n_samples[i], 0, out[i], out_cap[i], 0, frame_bytes ? frame_bytes[i] : nullptr};
+    }
+    const int rc = encode_pipelined(c, segs.data(), n);
+    resolve_timing(c);
+    for (uint32_t i = 0; i < n; i++) out_len[i] = rc ? 0 : segs[i].written;
+    return rc;
+}
+
+extern "C" {
 
 int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
                           uint64_t first_frame_number, uint8_t *out, size_t out_cap, size_t *out_len,
@@ -919,9 +988,10 @@ int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sa
     size_t written = 0;
     if (c->records_on) c->h_records.clear();
     if (!c->records_on && c->max_frames >= 2 && total_frames > std::min<uint64_t>(c->max_frames / 2u, 2048u)) {
-        const int rc = encode_frames_pipelined(c, src, n_samples, first_frame_number, out, out_cap, out_len,
-                                               frame_bytes);
+        PipeSeg seg{src, n_samples, first_frame_number, out, out_cap, 0, frame_bytes};
+        const int rc = encode_pipelined(c, &seg, 1);
         resolve_timing(c);
+        if (rc == FLACGPU_OK) *out_len = seg.written;
         return rc;
     }
     (void)stride;

@@ -11,7 +11,7 @@ constexpr int kLaneSamples = 64;   // samples per lane: one wave == one 4096-sam
 constexpr int kMaxPartOrder = 8;   // rice.MAX_ORDER (rice.zig:13)
 constexpr int kParamBytes = 512;   // params of all orders 0..8: offset (1<<o)-1 (511 used)
 constexpr int kCrcThreadsMax = 512;
-constexpr uint32_t kCtrSet = 16;    // u32 tickets per work_ctr set (reset_analysis_tickets)
+constexpr uint32_t kCtrSet = 32;    // u32 tickets per work_ctr set (reset_analysis_tickets)
 constexpr uint32_t kMd5StreamsPerWg = 256;  // k_md5_streams workgroup size (one stream per lane)
 // LPC (build-defined extension; the reference has none, readme.md:27): orders
 // 1..12 on the GPU path (the FLAC subset limit), 15-bit coefficients.

@@ -580,7 +580,7 @@ __device__ __forceinline__ void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n
 
 // Frame-queue tickets (EncodeArgs::work_ctr, one set of kCtrSet u32 per overlapped range):
 // [0] analysis full, [1] analysis tail, [2] pack full, [3] pack tail, [8..15] the split
-// analysis's per-XCD queues.  Each stage zeroes the other stage's tickets at its start (the
+// analysis's per-XCD queues, [16..23] the split pack's.  Each stage zeroes the other stage's tickets at its start (the
 // launches of one set are ordered), so no memset precedes a launch.
 __device__ __forceinline__ void reset_analysis_tickets(uint32_t *ctr, uint32_t tid) {
     if (blockIdx.x == 0 && tid < 16u && (tid < 2u || tid >= 8u)) ctr[tid] = 0u;
@@ -1214,6 +1214,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     // while frame i is analysed, so issuing frame i+1's DMA never waits on a global load.
     uint32_t *ctr = a.work_ctr + (FULL ? 0u : 1u);
     if (blockIdx.x == 0 && tid == 0) a.work_ctr[2] = a.work_ctr[3] = 0u;  // the pack kernel's queues
+    if (blockIdx.x == 0 && tid < 8u) a.work_ctr[16u + tid] = 0u;  // ... and its per-XCD split queues
     // Channel halves (a.ch_split, full frames of 4+ independent channels staged single-buffered):
     // a work item is (frame, half); the half's C channels are dwords [half drh, half drh + drh)
     // of every 2 drh-dword interchannel row, so two or three workgroups share a CU where one

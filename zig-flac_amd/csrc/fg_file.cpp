@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/flacgpu.h"
+#include "fg_internal.hpp"
 #include "fg_md5_host.hpp"
 
 namespace {
@@ -197,6 +198,87 @@ int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sa
     flacgpu_header_bytes(&si, 0, out);
     flacgpu_vorbis_comment_bytes(1, out + 42);
     *out_len = 73 + frames_len;
+    return FLACGPU_OK;
+}
+
+// wav2flac for n files at once on one context: every file's frames through ONE pipelined
+// H2D / encode / D2H schedule (fg::ctx_encode_segments: the pipeline runs on from file to file;
+// one context's streams, not one context per file contending for the GPU's hardware queues),
+// and every file's MD5 on the host hashing pool in one batch beside it (md5_pool_update_many:
+// up to four chains per core).  Each out[i] receives exactly what flacgpu_encode_file writes.
+int flacgpu_encode_files(flacgpu_ctx *ctx, uint32_t n_files, const void *const *pcm, uint32_t bytes_per_sample,
+                         const uint64_t *n_samples, uint8_t *const *out, const size_t *out_cap, size_t *out_len) {
+    if (!ctx || (n_files && (!pcm || !n_samples || !out || !out_cap || !out_len))) return FLACGPU_ERR_INVALID_INPUT;
+    flacgpu_config cfg;
+    int rc = flacgpu_get_config(ctx, &cfg);
+    if (rc) return rc;
+    if (bytes_per_sample != cfg.bits_per_sample / 8u) return FLACGPU_ERR_INVALID_INPUT;
+    for (uint32_t i = 0; i < n_files; i++) {
+        out_len[i] = 0;
+        if (!out[i] || (!pcm[i] && n_samples[i])) return FLACGPU_ERR_INVALID_INPUT;
+    }
+    for (uint32_t i = 0; i < n_files; i++)
+        if (out_cap[i] < 73) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
+    std::vector<fg::HostMd5> md5;
+    std::vector<fg::HostMd5 *> hp;
+    std::vector<const uint8_t *> src;
+    std::vector<size_t> bytes, caps, lens;
+    std::vector<uint8_t *> frames_out;
+    std::vector<std::vector<uint32_t>> sizes;
+    std::vector<uint32_t *> sizes_p;
+    try {
+        md5.resize(n_files);
+        hp.resize(n_files);
+        src.resize(n_files);
+        bytes.resize(n_files);
+        caps.resize(n_files);
+        lens.resize(n_files);
+        frames_out.resize(n_files);
+        sizes.resize(n_files);
+        sizes_p.resize(n_files);
+        for (uint32_t i = 0; i < n_files; i++) {
+            hp[i] = &md5[i];
+            src[i] = (const uint8_t *)pcm[i];
+            bytes[i] = (size_t)(n_samples[i] * cfg.channels * bytes_per_sample);
+            caps[i] = out_cap[i] - 73;
+            frames_out[i] = out[i] + 73;
+            sizes[i].resize((n_samples[i] + cfg.block_size - 1) / cfg.block_size + 1);
+            sizes_p[i] = sizes[i].data();
+        }
+    } catch (...) {
+        return FLACGPU_ERR_OUT_OF_MEMORY;
+    }
+    const bool host_md5 = flacgpu_md5_get_engine(ctx) == FLACGPU_MD5_HOST;
+    std::thread hasher;
+    if (host_md5) {
+        try {
+            hasher = std::thread([&]() { fg::md5_pool_update_many(hp.data(), src.data(), bytes.data(), n_files); });
+        } catch (const std::system_error &) {
+            fg::md5_pool_update_many(hp.data(), src.data(), bytes.data(), n_files);  // before the encode
+        }
+    }
+    rc = fg::ctx_encode_segments(ctx, n_files, src.data(), n_samples, frames_out.data(), caps.data(), lens.data(),
+                                 sizes_p.data());
+    if (hasher.joinable()) hasher.join();
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n_files; i++) {
+        flacgpu_streaminfo si;
+        flacgpu_streaminfo_init(&si, cfg.sample_rate, cfg.channels, cfg.bits_per_sample, n_samples[i], cfg.block_size);
+        const uint64_t nf = (n_samples[i] + cfg.block_size - 1) / cfg.block_size;
+        for (uint64_t f = 0; f < nf; f++) flacgpu_streaminfo_update_frame_size(&si, sizes[i][f]);
+        if (host_md5) {
+            md5[i].final(si.md5);
+        } else {
+            if ((rc = flacgpu_md5_init(ctx)) || (rc = flacgpu_md5_update(ctx, pcm[i], bytes[i])) ||
+                (rc = flacgpu_md5_final(ctx, si.md5))) {
+                for (uint32_t j = 0; j < n_files; j++) out_len[j] = 0;
+                return rc;
+            }
+        }
+        flacgpu_header_bytes(&si, 0, out[i]);
+        flacgpu_vorbis_comment_bytes(1, out[i] + 42);
+        out_len[i] = 73 + lens[i];
+    }
     return FLACGPU_OK;
 }
 

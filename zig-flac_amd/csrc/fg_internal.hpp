@@ -14,6 +14,11 @@ int ctx_encode_chunk(flacgpu_ctx *c, const uint8_t *src, uint64_t ns, uint64_t f
                      uint32_t *frame_bytes);
 // Copy the last chunk's `total` encoded bytes to host memory at out.
 int ctx_download_chunk(flacgpu_ctx *c, uint8_t *out, uint64_t total);
+// n independent streams from host memory, frames numbered from 0 each, through one pipelined
+// H2D / encode / D2H schedule that runs on from one stream into the next; out_len[i] = bytes of
+// stream i's frames at out[i], frame_bytes[i] (array and entries may be NULL) their sizes.
+int ctx_encode_segments(flacgpu_ctx *c, uint32_t n, const uint8_t *const *src, const uint64_t *n_samples,
+                        uint8_t *const *out, const size_t *out_cap, size_t *out_len, uint32_t *const *frame_bytes);
 uint32_t ctx_max_frames(const flacgpu_ctx *c);
 void ctx_finish(flacgpu_ctx *c);  // fold pending timing events
 }  // namespace fg

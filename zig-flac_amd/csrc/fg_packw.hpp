@@ -118,10 +118,23 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
 
     uint32_t *ctr = a.work_ctr + 2u;
     reset_analysis_tickets(a.work_ctr, tid);  // the analysis kernel's queues
-    if (tid == 0) misc[21] = gridDim.x + atomicAdd(ctr, 1u);
+    // split: items from per-XCD queues (work_ctr[16..23], zeroed by the analysis kernel), so the
+    // two halves of a frame -- which fetch the same lines of its interleaved rows -- are taken
+    // by workgroups of one XCD at about the same time and the second fetch can hit its L2
+    // (the analysis's xcd_ticket placement; tools/micro/fetch_micro.hip: 2.0x -> 1.28x)
+    const bool xq = SPLIT && a.xcd_queue;
+    uint32_t *xqc = a.work_ctr + 16;
+    if (tid == 0) {
+        if (xq) {
+            misc[22] = xcd_ticket(xqc, a.n_jobs);
+            misc[21] = xcd_ticket(xqc, a.n_jobs);
+        } else {
+            misc[21] = gridDim.x + atomicAdd(ctr, 1u);
+        }
+    }
     __syncthreads();
     const uint32_t n_items = a.n_jobs << ssh;
-    uint32_t jidx = blockIdx.x, buf = 0;
+    uint32_t jidx = xq ? (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[22]) : blockIdx.x, buf = 0;
     uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
     FrameJob job{}, jn{};
     if (jidx < n_items) job = a.jobs[jidx >> ssh];
@@ -135,7 +148,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     while (jidx < n_items) {
         const uint32_t l = opaque(l0);
         const uint32_t half = jidx & ssh;
-        if (tid == 0) misc[20] = gridDim.x + atomicAdd(ctr, 1u);
+        if (tid == 0) misc[20] = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
         uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
         // single buffer: the frame's DMA first, so the descriptor's dependent loads below run

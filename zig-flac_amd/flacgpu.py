@@ -243,6 +243,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_header_bytes": (SZ, [ctypes.POINTER(StreamInfo), I32, P]),
         "flacgpu_vorbis_comment_bytes": (SZ, [I32, P]),
         "flacgpu_encode_file": (I32, [P, P, U32, U64, P, SZ, ctypes.POINTER(SZ)]),
+        "flacgpu_encode_files": (I32, [P, U32, P, U32, P, P, P, P]),
         "flacgpu_wav_to_flac": (I32, [I32, P, SZ, P, SZ, ctypes.POINTER(SZ)]),
         "flacgpu_open_multi": (I32, [I32, P, ctypes.POINTER(Config), U32, ctypes.POINTER(P)]),
         "flacgpu_close_multi": (None, [P]),
@@ -275,7 +276,7 @@ def exported_symbols() -> list:
         "flacgpu_set_timing",
         "flacgpu_kernel_time", "flacgpu_reset_timing", "flacgpu_set_records", "flacgpu_set_overlap", "flacgpu_get_records",
         "flacgpu_get_config", "flacgpu_wav_parse", "flacgpu_streaminfo_init", "flacgpu_streaminfo_update_frame_size",
-        "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file",
+        "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file", "flacgpu_encode_files",
         "flacgpu_wav_to_flac", "flacgpu_open_multi", "flacgpu_close_multi", "flacgpu_multi_encode_frames",
     ]
 
@@ -410,6 +411,25 @@ class Encoder:
         _check(self.lib.flacgpu_encode_file(self.ctx, src, self.bytes_per_sample, n, out, cap, ctypes.byref(out_len)),
                "encode_file")
         return out.raw[: out_len.value]
+
+    def encode_files(self, pcms: Sequence[bytes]) -> list:
+        """flacgpu_encode_files: encode_file of every buffer, in one call (one pipelined schedule,
+        the MD5s batched on the host pool)."""
+        per = self.channels * self.bytes_per_sample
+        n = len(pcms)
+        ns = [len(p) // per for p in pcms]
+        caps = [200 + ((k + self.block_size - 1) // self.block_size) * self.frame_bound() for k in ns]
+        outs = [ctypes.create_string_buffer(c) for c in caps]
+        srcs = [ctypes.create_string_buffer(bytes(p), len(p)) if p else None for p in pcms]
+        src_p = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_void_p).value if b is not None else None
+                                                 for b in srcs])
+        out_p = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_void_p).value for b in outs])
+        ns_a = (ctypes.c_uint64 * max(n, 1))(*ns)
+        cap_a = (ctypes.c_size_t * max(n, 1))(*caps)
+        len_a = (ctypes.c_size_t * max(n, 1))()
+        _check(self.lib.flacgpu_encode_files(self.ctx, n, src_p, self.bytes_per_sample, ns_a, out_p, cap_a, len_a),
+               "encode_files")
+        return [outs[i].raw[: len_a[i]] for i in range(n)]
 
     def write_frame(self, planes, frame_number: int) -> bytes:
         """Encoder.writeFrame: planar int32 samples (C x n) -> one frame."""
