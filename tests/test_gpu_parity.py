@@ -230,6 +230,25 @@ def test_pack_split_matches_whole_frame(monkeypatch, ch, bits, rate):
     assert outs[0][1] == ref_sizes and outs[0][0] == ref, _diff_msg(outs[0][0], ref)
 
 
+@pytest.mark.parametrize("knobs", [{"FLACGPU_SPLIT_JIT": "1"}, {"FLACGPU_SPLIT_JIT": "1", "FLACGPU_PACK_XCDQ": "0"},
+                                   {"FLACGPU_XCD_QUEUE": "0", "FLACGPU_PACK_XCDQ": "0"}])
+def test_split_item_schedules_match_oracle(monkeypatch, knobs):
+    """The channel-half items of the split analysis and pack (c4) taken just in time from the
+    per-XCD queues (FLACGPU_SPLIT_JIT=1), or ahead from them, or from one global ticket: the
+    schedule only moves work between workgroups, the bytes are the restatement's."""
+    import flacgpu
+
+    ch, bits, rate = 8, 24, 96000
+    n = 4096 * 300 + 333  # enough items that every XCD queue runs dry and hands over
+    pcm = synth.synth_pcm(n, ch, bits, rate, stream=12)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    with flacgpu.Encoder(ch, bits, rate, max_frames=512) as enc:
+        out, sizes = enc.encode_frames(pcm)
+    ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, ch, bits, rate)
+    assert sizes == ref_sizes and out == ref, _diff_msg(out, ref)
+
+
 @pytest.mark.parametrize("cfg,max_frames,n", [
     ((2, 16, 44100), 8, 4096 * 37 + 1001),   # 4-frame chunks: 10 chunks, both halves reused 5x, a tail
     ((2, 24, 96000), 6, 4096 * 13),          # 3-frame chunks, no tail

@@ -138,6 +138,7 @@ struct flacgpu_ctx {
     uint32_t ovl_chunks = 0, ovl_ana = 2, ovl_pack = 2, ovl_min_frames = 4096;
     bool xcd_queue = true;  // split analysis: per-XCD item queues (fg_device.hpp xcd_ticket)
     bool pack_xcdq = true;  // split pack: the same (fg_packw.hpp)
+    bool split_jit = false;  // split analysis: each item's ticket taken right before its DMA
     // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp): analysis and pack in
     // one kernel, frame offsets by an in-kernel look-back over per-slot status words
     bool fused = false;
@@ -328,7 +329,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
         if (c->ana_split) {
             h.channels = c->C / 2u;
             h.ch_split = 1;
-            h.xcd_queue = c->xcd_queue ? 1u : 0u;
+            h.xcd_queue = c->xcd_queue ? (c->split_jit ? 3u : 1u) : 0u;
             HIPCHK(launch_stage(0, h, true, c->nt_split, c->lds_split, s));
             HIPCHK(launch_frame_totals(h, s));
         } else if (c->ana1) {
@@ -352,7 +353,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
             h.image_bytes = c->image_split;
             h.crc_pow4 = c->d_crc_pows;
             h.crc_hmax4 = c->crc_hmaxs;
-            h.xcd_queue = c->pack_xcdq ? 1u : 0u;
+            h.xcd_queue = c->pack_xcdq ? (c->split_jit ? 3u : 1u) : 0u;
             HIPCHK(launch_stage(1, h, true, c->nt_psplit, c->lds_psplit, s));
         } else if (c->nt_pack4) {
             HIPCHK(launch_stage(1, h, true, c->nt_pack4, c->lds_pack4, s));
@@ -663,6 +664,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (const char *e = std::getenv("FLACGPU_OVERLAP")) c->ovl_chunks = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_XCD_QUEUE")) c->xcd_queue = e[0] != '0';  // A/B knob
     if (const char *e = std::getenv("FLACGPU_PACK_XCDQ")) c->pack_xcdq = e[0] != '0';   // A/B knob
+    if (const char *e = std::getenv("FLACGPU_SPLIT_JIT")) c->split_jit = e[0] == '1';    // A/B knob
     if (const char *e = std::getenv("FLACGPU_OVL_ANA")) c->ovl_ana = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_OVL_PACK")) c->ovl_pack = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_OVL_MIN")) c->ovl_min_frames = (uint32_t)std::max(1, std::atoi(e));

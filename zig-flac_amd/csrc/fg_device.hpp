@@ -1222,6 +1222,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     // k_frame_totals after the launch.  The items come from the per-XCD queues (xcd_ticket).
     const uint32_t ssh = (FULL && a.ch_split) ? 1u : 0u;
     const bool xq = ssh && a.xcd_queue;
+    // jit (xcd_queue bit 1): the item's ticket is taken right before its DMA, not two items
+    // ahead, so the two halves of a frame -- consecutive items of one XCD's queue -- are staged
+    // about one ticket interval apart and the second fetch finds the first's lines in that
+    // XCD's L2 (taken ahead, the stagings are up to an item's duration apart: ~30 MB of other
+    // traffic through a 4-MB L2 in between)
+    const bool jit = xq && !dbuf && (a.xcd_queue & 2u);
     uint32_t *xqc = a.work_ctr + 8;
     const uint32_t drh = ssh ? C * (uint32_t)B / 4u : 0u;
     const uint32_t n_items = a.n_jobs << ssh;
@@ -1232,7 +1238,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             misc[22] = atomicAdd(ctr, 1u);
         } else if (xq) {
             misc[22] = xcd_ticket(xqc, a.n_jobs);
-            misc[21] = xcd_ticket(xqc, a.n_jobs);
+            misc[21] = jit ? 0xFFFFFFFFu : xcd_ticket(xqc, a.n_jobs);
         } else {
             misc[22] = blockIdx.x;
             misc[21] = gridDim.x + atomicAdd(ctr, 1u);
@@ -1250,7 +1256,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     // estimate barrier (step 9).  Taken after the DMA of the next frame's PCM, the wait for the
     // atomic's value also waited for that DMA.
     uint32_t tk = 0;
-    if (!FP && tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
+    if (!FP && !jit && tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
     while (jidx < n_items) {
         const uint32_t l = opaque(l0);  // keeps lane-derived addresses from being hoisted out of the loop
         const uint32_t half = jidx & ssh;
@@ -1893,7 +1899,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         uint32_t nn = 0;
         FrameJob jnn{};
         if constexpr (!FP) {
-            nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+            nn = jit ? 0xFFFFFFFFu : (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
             if (nn < n_items) jnn = a.jobs[nn >> ssh];
         }
         uint32_t channel_code, n_out;
@@ -2158,6 +2164,16 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             continue;
         }
         if (!dbuf) __syncthreads();
+        if (jit) {
+            // the next item's ticket now (single-buffered split staging: nothing is in flight)
+            if (tid == 0) misc[22] = xcd_ticket(xqc, a.n_jobs);
+            __syncthreads();
+            jidx = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[22]);
+            if (jidx < n_items) job = a.jobs[jidx >> ssh];
+            buf ^= 1u;
+            STAMP(6);
+            continue;
+        }
         if (tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
         STAMP(6);
         jidx = nxt; job = jn; nxt = nn; jn = jnn;

@@ -123,11 +123,14 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     // by workgroups of one XCD at about the same time and the second fetch can hit its L2
     // (the analysis's xcd_ticket placement; tools/micro/fetch_micro.hip: 2.0x -> 1.28x)
     const bool xq = SPLIT && a.xcd_queue;
+    // jit (xcd_queue bit 1, single-buffered staging): each item's ticket right before its DMA,
+    // as k_analyze's split mode, so a frame's halves are staged about one ticket interval apart
+    const bool jit = xq && !dbuf && (a.xcd_queue & 2u);
     uint32_t *xqc = a.work_ctr + 16;
     if (tid == 0) {
         if (xq) {
             misc[22] = xcd_ticket(xqc, a.n_jobs);
-            misc[21] = xcd_ticket(xqc, a.n_jobs);
+            misc[21] = jit ? 0xFFFFFFFFu : xcd_ticket(xqc, a.n_jobs);
         } else {
             misc[21] = gridDim.x + atomicAdd(ctr, 1u);
         }
@@ -148,7 +151,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     while (jidx < n_items) {
         const uint32_t l = opaque(l0);
         const uint32_t half = jidx & ssh;
-        if (tid == 0) misc[20] = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
+        if (tid == 0 && !jit) misc[20] = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
         uint32_t *stg = (uint32_t *)(smem + (buf ? LY.buf1 : LY.buf0));
         uint32_t *img = stg;  // the image reuses the staging buffer once the samples are in VGPRs
         // single buffer: the frame's DMA first, so the descriptor's dependent loads below run
@@ -199,7 +202,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         STAMP(8);
         __syncthreads();
         STAMP(0);
-        const uint32_t nn = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
+        const uint32_t nn = jit ? 0xFFFFFFFFu : (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
         // the job record of the frame after next before the DMA: waiting for it then never
         // waits for the DMA (vmcnt completes in order)
         FrameJob jnn{};
@@ -210,6 +213,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         if (skip) {
             if (tid == 0) atomicOr(a.err, fbytes + 16u > a.image_bytes ? 1u : 2u);
             __syncthreads();
+            if (jit) {
+                if (tid == 0) misc[22] = xcd_ticket(xqc, a.n_jobs);
+                __syncthreads();
+                jidx = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[22]);
+                if (jidx < n_items) job = a.jobs[jidx >> ssh];
+                continue;
+            }
             jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
             continue;
         }
@@ -507,6 +517,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         // single buffer: the next frame's staging overwrites the image
         if (!dbuf) __syncthreads();
         STAMP(6);
+        if (jit) {
+            if (tid == 0) misc[22] = xcd_ticket(xqc, a.n_jobs);
+            __syncthreads();
+            jidx = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[22]);
+            if (jidx < n_items) job = a.jobs[jidx >> ssh];
+            continue;
+        }
         jidx = nxt; job = jn; nxt = nn; jn = jnn; buf ^= dbuf ? 1u : 0u;
     }  // persistent frame loop (k_packw)
 #ifdef FG_STAMPS
