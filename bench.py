@@ -437,7 +437,7 @@ def stream_curve(args, enc, d_pcm, buf, fb, dev):
     """Same blocks per step at S concurrent streams: the encode beside the per-stream MD5 chains,
     on the engine the plan picks (flacgpu_plan_md5_engine: the host pool for a few long chains, one
     GPU lane per stream above the crossover), MD5 verified at every point.  Near the crossover the
-    other engine is timed too (`other`), which is how DESIGN.md section 5c's crossover is measured."""
+    other engine is timed too (`other`), which is how DESIGN.md section 5.2's crossover is measured."""
     import flacgpu
 
     out = []

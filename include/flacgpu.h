@@ -237,7 +237,7 @@ int flacgpu_md5_many(uint32_t n, const void *const *data, const uint64_t *lens, 
 int flacgpu_md5_plan_host(const flacgpu_plan *plan, const void *h_pcm, flacgpu_md5_state *states, uint8_t *digests);
 /* The faster MD5 engine for this plan's segments: FLACGPU_MD5_HOST below the
  * stream-count crossover (a few long chains), FLACGPU_MD5_DEVICE above it (the
- * model and its measured constants: DESIGN.md section 5c). */
+ * model and its measured constants: DESIGN.md section 5.2). */
 int flacgpu_plan_md5_engine(const flacgpu_plan *plan);
 
 /* Synchronise hip_stream (NULL: the context's stream) and report the device-side

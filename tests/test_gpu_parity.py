@@ -230,12 +230,14 @@ def test_pack_split_matches_whole_frame(monkeypatch, ch, bits, rate):
     assert outs[0][1] == ref_sizes and outs[0][0] == ref, _diff_msg(outs[0][0], ref)
 
 
-@pytest.mark.parametrize("knobs", [{"FLACGPU_SPLIT_JIT": "1"}, {"FLACGPU_SPLIT_JIT": "1", "FLACGPU_PACK_XCDQ": "0"},
+@pytest.mark.parametrize("knobs", [{"FLACGPU_SPLIT_JIT": "3"}, {"FLACGPU_SPLIT_JIT": "0"},
+                                   {"FLACGPU_SPLIT_JIT": "1", "FLACGPU_PACK_XCDQ": "0"},
                                    {"FLACGPU_XCD_QUEUE": "0", "FLACGPU_PACK_XCDQ": "0"}])
 def test_split_item_schedules_match_oracle(monkeypatch, knobs):
     """The channel-half items of the split analysis and pack (c4) taken just in time from the
-    per-XCD queues (FLACGPU_SPLIT_JIT=1), or ahead from them, or from one global ticket: the
-    schedule only moves work between workgroups, the bytes are the restatement's."""
+    per-XCD queues (FLACGPU_SPLIT_JIT bit 0 analysis, bit 1 pack), or ahead from them, or from
+    one global ticket: the schedule only moves work between workgroups, the bytes are the
+    restatement's."""
     import flacgpu
 
     ch, bits, rate = 8, 24, 96000

@@ -13,3 +13,4 @@ print('e2e', e['value'], e['mode'], e['files'], e['output_ok'])
 for c in e['curve']: print(c['files'], c['value'], c['wall_ms'], c['md5_pool_alone_ms'], c['frames_alone_ms'], c['batch'])" gpurun_out/r4l_e2e.json
 AB_REPS=2 AB_ARGS="--frames 65536" tools/ab.sh r4l "c4" base:- jit:FLACGPU_SPLIT_JIT=1 || exit 1
 AB_REPS=1 AB_ARGS="--frames 65536" tools/ab.sh r4l "c5" base:- prio1:FLACGPU_MD5_PRIO=1 prio3:FLACGPU_MD5_PRIO=3 k2:FLACGPU_MD5_KERNEL=2 rsv:FLACGPU_MD5_RESERVE=1
+timeout -k 10 900 bash tools/run_stamps.sh

@@ -7,8 +7,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <new>
 #include <system_error>
 #include <thread>
@@ -89,6 +92,8 @@ struct flacgpu_ctx {
     bool pack_dbuf = false;
     hipStream_t stream = nullptr, aux = nullptr;
     hipStream_t dl = nullptr;  // download stream of the pipelined host-buffer path
+    hipStream_t up = nullptr;  // its upload stream (chunk i+1's upload beside chunk i's encode)
+    hipEvent_t up_done[2] = {nullptr, nullptr};  // a chunk set's upload landed (GPU-side waits)
     hipEvent_t fork = nullptr, join = nullptr;
     // host waits of the pipelined host-buffer path (two chunk sets, the download stream, the end):
     // blocking-sync events, so a waiting thread sleeps instead of spinning on a core the MD5 pool
@@ -138,7 +143,10 @@ struct flacgpu_ctx {
     uint32_t ovl_chunks = 0, ovl_ana = 2, ovl_pack = 2, ovl_min_frames = 4096;
     bool xcd_queue = true;  // split analysis: per-XCD item queues (fg_device.hpp xcd_ticket)
     bool pack_xcdq = true;  // split pack: the same (fg_packw.hpp)
-    bool split_jit = false;  // split analysis: each item's ticket taken right before its DMA
+    // split analysis (bit 0) / pack (bit 1): each item's ticket taken right before its DMA, so a
+    // frame's two halves are staged close together (c4 A/B r4l: analysis 5.03 -> 4.95 ms, pack
+    // unchanged)
+    uint32_t split_jit = 1;
     // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp): analysis and pack in
     // one kernel, frame offsets by an in-kernel look-back over per-slot status words
     bool fused = false;
@@ -329,7 +337,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
         if (c->ana_split) {
             h.channels = c->C / 2u;
             h.ch_split = 1;
-            h.xcd_queue = c->xcd_queue ? (c->split_jit ? 3u : 1u) : 0u;
+            h.xcd_queue = c->xcd_queue ? ((c->split_jit & 1u) ? 3u : 1u) : 0u;
             HIPCHK(launch_stage(0, h, true, c->nt_split, c->lds_split, s));
             HIPCHK(launch_frame_totals(h, s));
         } else if (c->ana1) {
@@ -353,7 +361,7 @@ int encode_core(flacgpu_ctx *c, const uint8_t *d_pcm, const FrameJob *d_jobs, ui
             h.image_bytes = c->image_split;
             h.crc_pow4 = c->d_crc_pows;
             h.crc_hmax4 = c->crc_hmaxs;
-            h.xcd_queue = c->pack_xcdq ? (c->split_jit ? 3u : 1u) : 0u;
+            h.xcd_queue = c->pack_xcdq ? ((c->split_jit & 2u) ? 3u : 1u) : 0u;
             HIPCHK(launch_stage(1, h, true, c->nt_psplit, c->lds_psplit, s));
         } else if (c->nt_pack4) {
             HIPCHK(launch_stage(1, h, true, c->nt_pack4, c->lds_pack4, s));
@@ -655,6 +663,10 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     const uint32_t pack_wgs = c->B == 4 ? 2u : 4u;
     c->pack_dbuf = pack_layout(c->C, c->B, c->image_bytes, true).total * pack_wgs <= 160u * 1024u;
     if (const char *e = std::getenv("FLACGPU_PACK_DBUF")) c->pack_dbuf = c->pack_dbuf && e[0] == '1';  // tuning knob
+    // 32-bit samples (c5): the 48-KiB three-chunk ring (kernel 2) -- same-box A/B r4m, 2 reps:
+    // c5 24.19-24.25k -> 24.67-24.68k MS/s (MD5 10.1 -> 9.5 ms, analysis 8.84 -> 8.58 ms beside
+    // it); c3 neutral, C2 -4 %, so the others keep kernel 1
+    if (c->B == 4u) c->md5_kernel = 2;
     if (const char *e = std::getenv("FLACGPU_MD5_KERNEL")) c->md5_kernel = std::atoi(e);  // A/B knob
     if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);      // A/B knob
     if (const char *e = std::getenv("FLACGPU_ENC_PRIO")) c->enc_prio = e[0] == '1' ? 1u : 0u;  // A/B knob
@@ -664,7 +676,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (const char *e = std::getenv("FLACGPU_OVERLAP")) c->ovl_chunks = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_XCD_QUEUE")) c->xcd_queue = e[0] != '0';  // A/B knob
     if (const char *e = std::getenv("FLACGPU_PACK_XCDQ")) c->pack_xcdq = e[0] != '0';   // A/B knob
-    if (const char *e = std::getenv("FLACGPU_SPLIT_JIT")) c->split_jit = e[0] == '1';    // A/B knob
+    if (const char *e = std::getenv("FLACGPU_SPLIT_JIT")) c->split_jit = (uint32_t)std::atoi(e) & 3u;  // A/B knob
     if (const char *e = std::getenv("FLACGPU_OVL_ANA")) c->ovl_ana = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_OVL_PACK")) c->ovl_pack = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_OVL_MIN")) c->ovl_min_frames = (uint32_t)std::max(1, std::atoi(e));
@@ -737,6 +749,9 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&c->dl, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    if (hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+    for (hipEvent_t &ev : c->up_done)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&c->ovl, hipStreamNonBlocking) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
@@ -833,18 +848,21 @@ void flacgpu_close(flacgpu_ctx *c) {
         if (e) hipEventDestroy(e);
     if (c->aux) hipStreamDestroy(c->aux);
     if (c->dl) hipStreamDestroy(c->dl);
+    if (c->up) hipStreamDestroy(c->up);
+    for (hipEvent_t e : c->up_done)
+        if (e) hipEventDestroy(e);
     if (c->ovl) hipStreamDestroy(c->ovl);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
 
-// Host buffers in, host buffers out, with the PCIe directions overlapped: the context's
-// device buffers split into two halves, chunk i+1 is uploaded and encoded on c->stream
-// while a worker thread downloads chunk i's frames on c->dl (pageable copies block the
-// issuing thread, so the two directions need two threads).  Output bytes and frame sizes
-// are identical to the sequential loop; only the schedule differs.  The input is a list of
-// segments (files, flacgpu_encode_files): chunks never span two, and the pipeline runs on
-// from one segment into the next instead of draining at each file's end.
+// Host buffers in, host buffers out, with both PCIe directions and the encode overlapped: the
+// context's device buffers split into two halves (chunk sets); chunk i+1 uploads on c->up while
+// chunk i encodes on c->stream and chunk i-1's frames download on c->dl, issued by one worker
+// thread (pageable copies block the issuing thread, so the download needs a thread of its own).
+// Output bytes and frame sizes are identical to the sequential loop; only the schedule differs.
+// The input is a list of segments (files, flacgpu_encode_files): chunks never span two, and the
+// pipeline runs on from one segment into the next instead of draining at each file's end.
 struct PipeSeg {
     const uint8_t *src;
     uint64_t n_samples, first_frame_number;
@@ -862,53 +880,93 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     const uint64_t pcm_half = (uint64_t)(c->max_frames / 2u) * kBlock * c->C * c->B;  // 16-B multiple
     const uint64_t out_half = (uint64_t)(c->max_frames / 2u) * c->image_bytes;
     const uint64_t fb_half = c->max_frames / 2u;
-    hipEvent_t *done = c->hw;  // chunk sets 0 and 1 (blocking-sync events)
-    int wrc = FLACGPU_OK;  // the worker's result
-    std::thread worker;
-    auto download = [&](int set, PipeSeg *sg, uint64_t frame0, uint64_t nf) {
-        wrc = FLACGPU_OK;
-        if (hipSetDevice(c->device) != hipSuccess || hipEventSynchronize(done[set]) != hipSuccess) {
-            wrc = FLACGPU_ERR_DEVICE;
-            return;
-        }
+    hipEvent_t *done = c->hw;  // a chunk set's encode finished (blocking-sync events)
+    struct Dl {
+        int set;
+        PipeSeg *sg;
+        uint64_t frame0, nf;
+    };
+    // the download worker: one thread for the whole call, fed chunk by chunk
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<Dl> q;
+    uint64_t n_done = 0;  // downloads finished (in chunk order)
+    bool closing = false;
+    int wrc = FLACGPU_OK;  // the first download error
+    auto download = [&](const Dl &d) -> int {
+        PipeSeg *sg = d.sg;
+        if (hipSetDevice(c->device) != hipSuccess || hipEventSynchronize(done[d.set]) != hipSuccess)
+            return FLACGPU_ERR_DEVICE;
         uint64_t total = 0;
-        if (hipMemcpyAsync(&total, c->d_total + set, 8, hipMemcpyDeviceToHost, c->dl) != hipSuccess ||
-            wait_host(c, c->dl, 2) != hipSuccess) {
-            wrc = FLACGPU_ERR_DEVICE;
-            return;
-        }
-        if (sg->written + total > sg->out_cap) {
-            wrc = FLACGPU_ERR_OUTPUT_TOO_SMALL;
-            return;
-        }
-        if ((sg->frame_bytes && hipMemcpyAsync(sg->frame_bytes + frame0, c->d_fbytes + set * fb_half, nf * 4,
+        if (hipMemcpyAsync(&total, c->d_total + d.set, 8, hipMemcpyDeviceToHost, c->dl) != hipSuccess ||
+            wait_host(c, c->dl, 2) != hipSuccess)
+            return FLACGPU_ERR_DEVICE;
+        if (sg->written + total > sg->out_cap) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
+        if ((sg->frame_bytes && hipMemcpyAsync(sg->frame_bytes + d.frame0, c->d_fbytes + d.set * fb_half, d.nf * 4,
                                                hipMemcpyDeviceToHost, c->dl) != hipSuccess) ||
-            hipMemcpyAsync(sg->out + sg->written, c->d_out + set * out_half, total, hipMemcpyDeviceToHost, c->dl) !=
+            hipMemcpyAsync(sg->out + sg->written, c->d_out + d.set * out_half, total, hipMemcpyDeviceToHost, c->dl) !=
                 hipSuccess ||
-            wait_host(c, c->dl, 2) != hipSuccess) {
-            wrc = FLACGPU_ERR_DEVICE;
-            return;
-        }
+            wait_host(c, c->dl, 2) != hipSuccess)
+            return FLACGPU_ERR_DEVICE;
         sg->written += total;
+        return FLACGPU_OK;
+    };
+    auto work = [&]() {
+        for (;;) {
+            Dl d;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return closing || !q.empty(); });
+                if (q.empty()) return;
+                d = q.front();
+                q.pop_front();
+            }
+            const int r = wrc == FLACGPU_OK ? download(d) : FLACGPU_OK;  // after an error: drain only
+            {
+                std::lock_guard<std::mutex> lk(m);
+                if (r != FLACGPU_OK && wrc == FLACGPU_OK) wrc = r;
+                n_done++;
+            }
+            cv.notify_all();
+        }
+    };
+    std::thread worker;
+    try {
+        worker = std::thread(work);
+    } catch (const std::system_error &) {
+        return FLACGPU_ERR_OUT_OF_MEMORY;
+    }
+    // wait (host) until at least `k` downloads have finished; the first download error
+    auto wait_done = [&](uint64_t k) -> int {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return n_done >= k || wrc != FLACGPU_OK; });
+        return wrc;
     };
     int rc = FLACGPU_OK;
-    int set = 0;
+    uint64_t chunk = 0;  // chunks issued so far
     for (size_t si = 0; si < nseg && rc == FLACGPU_OK; si++) {
         PipeSeg *sg = &segs[si];
         sg->written = 0;
         const uint64_t total_frames = frames_for(sg->n_samples, bs);
-        for (uint64_t frame0 = 0; frame0 < total_frames && rc == FLACGPU_OK; set ^= 1) {
+        for (uint64_t frame0 = 0; frame0 < total_frames && rc == FLACGPU_OK; chunk++) {
+            const int set = (int)(chunk & 1u);
             const uint64_t nf = std::min<uint64_t>(F, total_frames - frame0);
             const uint64_t s0 = frame0 * bs;
             const uint64_t ns = std::min<uint64_t>(nf * bs, sg->n_samples - s0);
             uint8_t *dp = c->d_pcm + set * pcm_half;
-            // chunk i - 1's download (worker) overlaps this upload; chunk i - 2 used this half
-            if (hipMemcpyAsync(dp, sg->src + s0 * c->C * c->B, ns * c->C * c->B, hipMemcpyHostToDevice, c->stream) !=
-                hipSuccess) {
+            // upload: the PCM half was last read by chunk i-2's encode (its `done` event, a GPU-side
+            // wait); it runs beside chunk i-1's encode and chunk i-2's download
+            if ((chunk >= 2 && hipStreamWaitEvent(c->up, done[set], 0) != hipSuccess) ||
+                hipMemcpyAsync(dp, sg->src + s0 * c->C * c->B, ns * c->C * c->B, hipMemcpyHostToDevice, c->up) !=
+                    hipSuccess ||
+                hipEventRecord(c->up_done[set], c->up) != hipSuccess) {
                 rc = FLACGPU_ERR_DEVICE;
                 break;
             }
-            if (launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, sg->first_frame_number + frame0, (uint32_t)nf,
+            // the encode writes the output half chunk i-2's download reads: that download first
+            if (chunk >= 2 && (rc = wait_done(chunk - 1))) break;
+            if (hipStreamWaitEvent(c->stream, c->up_done[set], 0) != hipSuccess ||
+                launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, sg->first_frame_number + frame0, (uint32_t)nf,
                                  c->stream) != hipSuccess) {
                 rc = FLACGPU_ERR_DEVICE;
                 break;
@@ -921,26 +979,23 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
                 rc = FLACGPU_ERR_DEVICE;
                 break;
             }
-            // chunk i - 1's download ran beside this chunk's upload and encode (the other half);
-            // it must end before the next worker (output order) and before half set ^ 1 is reused
-            if (worker.joinable()) {
-                worker.join();
-                if ((rc = wrc)) break;
+            {
+                std::lock_guard<std::mutex> lk(m);
+                q.push_back(Dl{set, sg, frame0, nf});
             }
-            try {
-                worker = std::thread(download, set, sg, frame0, nf);
-            } catch (const std::system_error &) {
-                download(set, sg, frame0, nf);  // no thread to be had: download in line
-                if ((rc = wrc)) break;
-            }
+            cv.notify_all();
             frame0 += nf;
         }
     }
-    if (worker.joinable()) {
-        worker.join();
-        if (rc == FLACGPU_OK) rc = wrc;
+    {
+        std::lock_guard<std::mutex> lk(m);
+        closing = true;
     }
+    cv.notify_all();
+    worker.join();
+    if (rc == FLACGPU_OK) rc = wrc;
     if (rc) {
+        hipStreamSynchronize(c->up);
         hipStreamSynchronize(c->stream);
         return rc;
     }
@@ -1220,7 +1275,7 @@ int flacgpu_md5_plan_host(const flacgpu_plan *p, const void *h_pcm, flacgpu_md5_
 int flacgpu_plan_md5_engine(const flacgpu_plan *p) {
     if (!p || !p->n_streams) return FLACGPU_MD5_DEVICE;
     // Time of each engine for the plan's segments, from the rates bench.py's stream_curve measured
-    // on MI355X (DESIGN.md section 5c): device -- one lane per stream at ~72 MB/s beside the encode,
+    // on MI355X (DESIGN.md section 5.2): device -- one lane per stream at ~72 MB/s beside the encode,
     // at most ~600 GB/s over the chip (16384 streams: 4.3 GB of MD5 in 7.1 ms); host -- the pool's
     // workers at ~0.95 GB/s a chain, k chains interleaved on a worker (k <= 4) running k / g(k)
     // times as long as one, g = 1, 1.7, 2.2, 2.6 (64 streams on 16 workers: 41 GB/s).
