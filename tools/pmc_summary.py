@@ -4,7 +4,8 @@ profiles/<tag>_summary.md and profiles/<tag>_pmc.json.
 
 HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE
 are kilobytes (x1024); on gfx950 FETCH_SIZE counts half the bytes of wide
-coalesced reads, so it is doubled.  Counters are averaged per dispatch of each
+coalesced reads, so it is doubled (calibrated for the 4-B LDS-DMA staging of the wide configs too:
+tools/micro/fetch_micro.hip, profiles/r4g_fetch_calib.json).  Counters are averaged per dispatch of each
 kernel family.
 
 Usage: tools/pmc_summary.py <prof_dir> <tag> <frames_per_launch> <workload key (bench.py workload_key)>
@@ -55,7 +56,8 @@ def main():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             hbm[fam] = round(cs["FETCH_SIZE"] * 1024 * 2 + cs["WRITE_SIZE"] * 1024)
     out = {"tag": tag, "workload": workload, "frames_per_launch": frames, "hbm_bytes_per_launch": hbm,
-           "fetch_note": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count correction) + WRITE_SIZE KiB x1024",
+           "fetch_note": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count correction: the guide's 16-B loads, and "
+                         "4-B LDS-DMA calibrated in profiles/r4g_fetch_calib.json) + WRITE_SIZE KiB x1024",
            "kernel_stats": stats, "counters_per_dispatch": avg}
     os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
     json.dump(out, open(os.path.join(root, "profiles", f"{tag}_pmc.json"), "w"), indent=1)

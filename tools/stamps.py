@@ -5,8 +5,9 @@ sys.path.insert(0, os.path.join(ROOT, "zig-flac_amd"))
 import numpy as np, torch
 import flacgpu, synth
 
-NAMES = ["DMA issue+job load", "sample load", "waste+eq", "bestOrder", "rice pass", "param search", "desc+rec+bar",
-         "stereo+exact", "ticket atomic", "vmcnt(0) wait", "top barrier"]
+NAMES = ["DMA issue+job load", "sample load", "waste+eq", "bestOrder", "rice pass", "param search (rest)",
+         "desc+rec+bar", "stereo+exact", "ticket atomic", "vmcnt(0) wait", "top barrier",
+         "fixed rice search", "LPC load+autocorr", "LPC Levinson-Durbin", "LPC residual pass"]
 PNAMES = ["top barrier", "offsets+bar", "zero img+bars", "residuals", "pack codes+bar", "CRC+bars", "store+bar",
           "ticket+desc loads", "vmcnt(0) wait", "DMA issue+sample load", "lane_bits/bits loads+scan"]
 S, F = 1024, 32

@@ -14,6 +14,7 @@
 // fg_enc_b{1,2,3,4}.hip.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <mutex>
 #include <type_traits>
 
@@ -1773,6 +1774,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             ltab = (int32_t *)(smem + LY.lpc) + wave * (uint32_t)kLpcTab;
             const uint32_t Q = a.lpc_order;
             if (lpc_on && R.type != 0 && n > Q) {
+                STAMP(11);  // (stamps build: the fixed predictor's search ends here)
                 bool fits;
                 uint32_t qsel = 0;  // the order selected by its LD error (contract step 7)
                 {
@@ -1781,8 +1783,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     if (fits) {
                         int64_t Rac[LPW + 1];
                         lpc_autocorr<LPW, int32_t>(x, n, l, Rac);
+                        STAMP(12);
                         __builtin_amdgcn_sched_barrier(0);
                         qsel = lpc_coefs<LPW>(Rac, Q, ltab, l, n, bps);
+                        STAMP(13);
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1826,6 +1830,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                                 else lpc_fast_pass<LPW, LPW>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
                                 const uint32_t tall = (uint32_t)__builtin_amdgcn_readfirstlane(
                                     (int)wave_or32(T8[0] | T8[1] | T8[2] | T8[3]));
+                                STAMP(14);
                                 if (tall >= (1u << 30)) continue;  // some residual outside [-2^30, 2^30)
                                 // OR of the zigzags' bit lengths: zz = 2t + sign
                                 uint32_t O8[4];
@@ -2181,7 +2186,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     }  // persistent frame loop
 #ifdef FG_STAMPS
     if (l0 == 0 && a.stamps)
-        for (int i = 0; i < 11; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
+        for (int i = 0; i < 16; i++) atomicAdd(&a.stamps[i], (unsigned long long)ph_[i]);
 #endif
 }
 
@@ -2627,6 +2632,14 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
     }
     if (a.channels == 2) FG_L(2, 256);
     if (a.channels == 1) FG_L(1, 256);
+    // four channels (the channel halves of 8-channel frames, c4): compile-time C halves the
+    // analysis's spills (VGPR 43 -> 22, SGPR 368 -> 128, scratch 112 -> 64 B per lane); the
+    // pack keeps the runtime form (its NC = 4 build spills where NC = 0 does not)
+    if constexpr (LPW == 0) {
+        static const bool nc4 = !std::getenv("FLACGPU_NC4") || std::getenv("FLACGPU_NC4")[0] != '0';  // A/B knob
+        if (nc4 && stage == 0 && full && a.channels == 4 && threads == 256u)
+            return launch_persistent(k_analyze<B, CLS, true, 256, 4, 0>, a, threads, lds, st);
+    }
     if (threads <= 256) FG_L(0, 256);
     FG_L(0, 512);
 #undef FG_L
