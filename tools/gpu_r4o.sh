@@ -7,3 +7,4 @@ timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; echo "gpu tests rc=$rc"; tail -2 gpurun_out/r4o_parity.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r4o_parity.log | head; exit $rc; }
 AB_REPS=2 AB_ARGS="--frames 65536" tools/ab.sh r4o "c4" nc4:- rt:FLACGPU_NC4=0 jit3:FLACGPU_SPLIT_JIT=3
+AB_REPS=2 tools/ab.sh r4o "c2" fused:- unfused:lib=zig-flac_amd/build_x

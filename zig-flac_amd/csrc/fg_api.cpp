@@ -144,8 +144,8 @@ struct flacgpu_ctx {
     bool xcd_queue = true;  // split analysis: per-XCD item queues (fg_device.hpp xcd_ticket)
     bool pack_xcdq = true;  // split pack: the same (fg_packw.hpp)
     // split analysis (bit 0) / pack (bit 1): each item's ticket taken right before its DMA, so a
-    // frame's two halves are staged close together (c4 A/B r4l: analysis 5.03 -> 4.95 ms, pack
-    // unchanged)
+    // frame's two halves are staged close together (c4 A/B r4l: analysis 5.03 -> 4.95 ms, analysis
+    // traffic 1.82x -> 1.44x of the PCM (r4n); the pack's bit measured no gain, r4o)
     uint32_t split_jit = 1;
     // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp): analysis and pack in
     // one kernel, frame offsets by an in-kernel look-back over per-slot status words

@@ -1228,7 +1228,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     // about one ticket interval apart and the second fetch finds the first's lines in that
     // XCD's L2 (taken ahead, the stagings are up to an item's duration apart: ~30 MB of other
     // traffic through a 4-MB L2 in between)
-    const bool jit = xq && !dbuf && (a.xcd_queue & 2u);
+    const bool jit = NC != 1 && NC != 2 && xq && !dbuf && (a.xcd_queue & 2u);  // (split: 4+ channels only)
     uint32_t *xqc = a.work_ctr + 8;
     const uint32_t drh = ssh ? C * (uint32_t)B / 4u : 0u;
     const uint32_t n_items = a.n_jobs << ssh;
@@ -1379,7 +1379,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // Full 16-bit frames: bestOrder accumulates |e_q| per 16-sample group (the finest Rice
         // partitions) for every order, so the chosen order's partition sums come out of it and
         // the second residual pass only ORs zigzags (the escape widths).
-        constexpr bool FUSED = FULL && CLS == 16;
+#ifndef FG_BO_FUSED
+#define FG_BO_FUSED 1
+#endif
+        constexpr bool FUSED = FULL && CLS == 16 && FG_BO_FUSED;
         uint32_t tg[5][4];
         if (try_fixed) {
             // ---- 5. bestOrder (fixed.zig:85-167)
