@@ -1382,6 +1382,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
 #ifndef FG_BO_FUSED
 #define FG_BO_FUSED 1
 #endif
+#ifndef FG_DESC_SUB
+#define FG_DESC_SUB 1  // two-channel builds: SubDesc fixed fields in one six-lane store (r4s: WRITE 0.68 -> 0.50 GB)
+#endif
+#ifndef FG_DESC_FRAME
+#define FG_DESC_FRAME 0  // two-channel builds: FrameDesc in one eight-lane store (r4s: no WRITE gain, off)
+#endif
         constexpr bool FUSED = FULL && CLS == 16 && FG_BO_FUSED;
         uint32_t tg[5][4];
         if (try_fixed) {
@@ -1398,6 +1404,13 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 for (int q = 0; q < 5; q++)
 #pragma unroll
                     for (int g = 0; g < 4; g++) tg[q][g] = 0;
+                // orders 3 and 4 of group 0 leave the registers when the group ends: to this wave's
+                // Rice parameter area (free until step 7) for the S8 pick, and into uniform partial
+                // sums for T -- two VGPRs fewer at the loop's end, where the compiler spilled one
+                // per frame (scratch writes)
+#define FG_ROWS64(v) ((uint64_t)rdl(v, 0) + rdl(v, 16) + rdl(v, 32) + rdl(v, 48))
+                uint32_t *stash = (uint32_t *)par;
+                uint64_t part3 = 0, part4 = 0;
 #pragma unroll
                 for (int j = 0; j < 64; j++) {
                     const int g = j >> 4;
@@ -1421,14 +1434,22 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                         tg[0][g] = n0; tg[1][g] = n1; tg[2][g] = n2; tg[3][g] = n3; tg[4][g] = n4;
                     }
                     pb0 = b0; pb1 = b1; pb2 = b2; pb3 = b3;
+                    if (!FP && j == 15) {
+                        stash[l] = tg[3][0];
+                        stash[64u + l] = tg[4][0];
+                        part3 = FG_ROWS64(row_sum32(tg[3][0]));
+                        part4 = FG_ROWS64(row_sum32(tg[4][0]));
+                        tg[3][0] = tg[4][0] = 0;
+                    }
                 }
                 // per lane <= 64 * 2^21: row sums (16 lanes) stay below 2^32
-#define FG_ROWS64(v) ((uint64_t)rdl(v, 0) + rdl(v, 16) + rdl(v, 32) + rdl(v, 48))
 #pragma unroll
                 for (int q = 0; q < 5; q++) {
                     const uint32_t r = row_sum32(tg[q][0] + tg[q][1] + tg[q][2] + tg[q][3]);
                     T[q] = FG_ROWS64(r);
                 }
+                T[3] += part3;
+                T[4] += part4;
 #undef FG_ROWS64
             } else if constexpr (CLS != 32) {
                 // biased differences b = e + 0x7FFFFFFF keep unsigned order == signed order:
@@ -1748,6 +1769,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
 #pragma unroll
                 for (int g = 0; g < 4; g++)
                     S8[g] = k == 0 ? tg[0][g] : k == 1 ? tg[1][g] : k == 2 ? tg[2][g] : k == 3 ? tg[3][g] : tg[4][g];
+                if (!FP && k >= 3) S8[0] = ((const uint32_t *)par)[(k == 3 ? 0u : 64u) + l];  // stashed above
                 auto acc = [&](int j, bool warm, SS r) { O8[j >> 4] |= warm ? 0u : zigzag32((int32_t)r); };
                 FG_DISPATCH_K(k, (residuals_k<K, SS>(s, hl1, hl2, hl3, hl4, l, acc)))
             } else {
@@ -1957,11 +1979,6 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 // samples from the staged PCM and recompute them.
                 const uint32_t o = R.porder, param_len = 4u + R.method, w = R.waste;
                 const uint8_t *pp = par + cur * 512u + ((1u << o) - PO);
-                if (l == 0) {
-                    const uint32_t p0 = pp[0];
-                    seg = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
-                    if (R.type == 3) seg += 4u + 5u + k * (uint32_t)kLpcPrec;  // precision, shift, coefficients
-                }
                 // residuals of the chosen predictor, recomputed from the staged PCM: fixed order k
                 // (fixed.zig:30-76) or the chosen LPC order from the coefficient table
                 auto pass = [&](auto &&f) {
@@ -2045,6 +2062,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     };
                     pass(len_a);
                 }
+                // the subframe header (lane 0), added after the pass: not held live through it
+                if (l == 0) {
+                    const uint32_t p0 = pp[0];
+                    seg += 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u);
+                    if (R.type == 3) seg += 4u + 5u + k * (uint32_t)kLpcPrec;  // precision, shift, coefficients
+                }
             }
         }
         const uint32_t sub_bits = wave_sum32(seg);
@@ -2067,7 +2090,21 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         }
         if (!FP && my_slot >= 0) {
             SubDesc *sd = (SubDesc *)(fd + sizeof(FrameDesc)) + my_slot;  // (split: the global channel)
-            if (l == 0) {
+            // the fixed fields (type .. lpc_shift, bits, lpc_prec, cval: bytes 0..23) as six dwords
+            // from lanes 0..5 -- one store instruction, one 32-B write, where eleven one-lane
+            // stores of 1-8 bytes were eleven partial-line writes per subframe (two-channel
+            // builds; the four-channel build spills twice as much with it, so it keeps the
+            // one-lane stores)
+            if constexpr (NC == 2 && FG_DESC_SUB) {
+                if (l < 6u) {
+                    const uint32_t w0 = R.type | (R.waste << 8) | (R.bd << 16) | (R.order << 24);
+                    const uint32_t w1 = R.porder | (R.method << 8) | (cand << 16) | ((uint32_t)(uint8_t)(int8_t)R.lsh << 24);
+                    const uint64_t cv = (uint64_t)R.cval;
+                    const uint32_t v = l == 0 ? w0 : l == 1 ? w1 : l == 2 ? sub_bits : l == 3 ? (uint32_t)kLpcPrec
+                                     : l == 4 ? (uint32_t)cv : (uint32_t)(cv >> 32);
+                    ((uint32_t *)sd)[l] = v;
+                }
+            } else if (l == 0) {
                 sd->type = (uint8_t)R.type;
                 sd->waste = (uint8_t)R.waste;
                 sd->bd = (uint8_t)R.bd;
@@ -2100,7 +2137,24 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             a.frame_bytes[job.slot] = fbytes;
             st_publish(a.status, job.slot, kStAgg | fbytes);  // before any wait (fg_fused.hpp)
         }
-        if (!FP && tid == 0 && half == 0) {
+        if (!FP && NC == 2 && FG_DESC_FRAME && wave == 0) {
+            // the FrameDesc (32 B) from lanes 0..7 in one store (two-channel builds, as above)
+            const uint32_t *hw = misc + 32;
+            const uint32_t hb = misc[18];
+            uint32_t total = 8u * hb;
+            for (uint32_t c = 0; c < n_out; c++) total += misc[40 + c];
+            if (l < 8u) {
+                const uint32_t v = l == 0 ? hb : l == 1 ? total : l == 2 ? channel_code : l == 3 ? n_out : hw[(l - 4u) & 3u];
+                ((uint32_t *)fd)[l] = v;
+            }
+            if (l == 0) {
+                const uint32_t fbytes = ((total + 7u) >> 3) + 2u;
+                if (fbytes + 16u > a.image_bytes) atomicOr(a.err, 1u);  // the pack kernel's image bound
+                a.frame_bytes[job.slot] = fbytes;
+                if (a.status) st_publish(a.status, job.slot, kStAgg | fbytes);  // fused launch follows
+                misc[17] = fbytes;
+            }
+        } else if (!FP && tid == 0 && half == 0) {
             const uint32_t *hw = misc + 32;
             const uint32_t hb = misc[18];
             FrameDesc *f = (FrameDesc *)fd;
