@@ -48,9 +48,12 @@ The JSON line also carries:
                    stream's MD5 on the engine the plan picks (host pool below the
                    crossover, one GPU lane per stream above), verified; both
                    engines timed near the crossover (rank 0, N = 1);
-  end_to_end    -- BASELINE.md's host-buffer contract: 8 ten-minute WAV-sized PCM
+  end_to_end    -- BASELINE.md's host-buffer contract: 8 .. 64 ten-minute WAV-sized PCM
                    buffers in host memory -> .flac files in host memory (H2D,
-                   kernels, D2H, MD5 on host threads, 73-byte header) (rank 0, N = 1);
+                   kernels, D2H, MD5 on the host pool, 73-byte header), per file
+                   (flacgpu_encode_file, one context + thread each) and as one
+                   flacgpu_encode_files call; bounds: the files' MD5 alone on the
+                   pool, the frames path alone (rank 0, N = 1);
   cpu_baseline  -- the CPU restatement (oracle/, "port", -O3) on P pinned host
                    threads over a bounded sample of the same workload.
 """

@@ -246,6 +246,24 @@ def test_host_md5_engine_matches_device_state_by_state():
         many.close()
 
 
+def test_host_md5_plan_rules():
+    """flacgpu_md5_plan_host's input rules match the device path's: no state with a non-final
+    segment is an error, an empty plan is a no-op on the device engine's side of the pick."""
+    import flacgpu
+
+    ch, bits, rate = 2, 16, 44100
+    with _encoder(ch, bits, rate, max_frames=8) as enc:
+        plan = enc.plan([0], [4096], final=[False])
+        buf = np.zeros(4096 * 4, dtype=np.uint8)
+        with pytest.raises(flacgpu.FlacGpuError):
+            plan.md5_host(buf.ctypes.data, None, None)  # nowhere to carry the chain
+        plan.close()
+        empty = enc.plan([], [])
+        assert empty.md5_engine() == flacgpu.MD5_DEVICE
+        empty.md5_host(buf.ctypes.data, None, None)
+        empty.close()
+
+
 def test_non_final_segment_must_be_whole_frames():
     import flacgpu
 
