@@ -1164,6 +1164,9 @@ __device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int3
 #define FG_PACK_MINW 4
 #endif
 
+#ifndef FG_JOB_LDS
+#define FG_JOB_LDS 1  // the next job records in an LDS ring instead of registers
+#endif
 #include "fg_fused.hpp"
 #include "fg_rice16.hpp"
 
@@ -1250,7 +1253,30 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
     uint32_t nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[21]);
     FrameJob job{}, jn{};
     if (jidx < n_items) job = a.jobs[jidx >> ssh];
-    if (nxt < n_items) jn = a.jobs[nxt >> ssh];
+    // FG_JOB_LDS: the next two job records ride in an LDS ring (misc[52..63], two 6-dword slots)
+    // filled by LDS-DMA from wave 0, instead of being held in registers through the frame; slot
+    // `ri` holds the next frame's, the other the one after it
+    constexpr bool JL = FG_JOB_LDS && !FP;
+    uint32_t *jring = misc + 52;
+    uint32_t ri = 0;
+    auto job_dma = [&](uint32_t idx, uint32_t slot) {
+        if (wave == 0 && l0 < 6u) lds_dma<4>((const uint32_t *)(a.jobs + (idx >> ssh)) + l0, jring + 6u * slot);
+    };
+    auto job_lds = [&](uint32_t slot) -> FrameJob {
+        FrameJob j;
+        const uint32_t *r = jring + 6u * slot;
+        j.pcm_off = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r[0]) |
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r[1]) << 32);
+        j.number = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r[2]) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r[3]) << 32);
+        j.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[4]);
+        j.slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[5]);
+        return j;
+    };
+    if (nxt < n_items) {
+        if constexpr (JL) job_dma(nxt, 0u);
+        else jn = a.jobs[nxt >> ssh];
+    }
     if (dbuf && jidx < n_items) stage_dma(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.stage0), cw, cst, wave, NW, l0, NC == 2 && B == 2, drh, jidx & ssh);
     // The ticket of the frame after next is taken at the END of the frame before (behind its
     // descriptor stores, which the top of the next frame waits for anyway) and published at the
@@ -1279,8 +1305,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         STAMP(9);
         __syncthreads();
         STAMP(10);
-        if (dbuf && nxt < n_items)
-            stage_dma(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l, NC == 2 && B == 2, drh, nxt & ssh);
+        if (dbuf && nxt < n_items) {
+            const uint64_t noff = JL ? job_lds(ri).pcm_off : jn.pcm_off;
+            stage_dma(a.pcm, noff, (uint32_t *)(smem + (buf ? LY.stage0 : LY.stage1)), cw, cst, wave, NW, l, NC == 2 && B == 2, drh, nxt & ssh);
+        }
         STAMP(0);
 
         // ---- 2. each wave loads its candidate: lane l owns samples [64l, 64l+64)
@@ -1930,7 +1958,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         FrameJob jnn{};
         if constexpr (!FP) {
             nn = jit ? 0xFFFFFFFFu : (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
-            if (nn < n_items) jnn = a.jobs[nn >> ssh];
+            if (nn < n_items) {
+                if constexpr (JL) job_dma(nn, ri ^ 1u);  // lands before the next frame's top barrier
+                else jnn = a.jobs[nn >> ssh];
+            }
         }
         uint32_t channel_code, n_out;
         int my_slot;
@@ -2238,7 +2269,14 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         }
         if (tid == 0) tk = xq ? xcd_ticket(xqc, a.n_jobs) : gridDim.x + atomicAdd(ctr, 1u);
         STAMP(6);
-        jidx = nxt; job = jn; nxt = nn; jn = jnn;
+        if constexpr (JL) {
+            if (nxt < n_items) job = job_lds(ri);  // DMA'd a frame ago, waited at this frame's top
+            ri ^= 1u;
+        } else {
+            job = jn;
+            jn = jnn;
+        }
+        jidx = nxt; nxt = nn;
         buf ^= 1u;
     }  // persistent frame loop
 #ifdef FG_STAMPS
