@@ -231,8 +231,8 @@ def test_cpp_encoder_api_matches_oracle_file(tmp_path, ch, bits, rate, n):
 
 @pytest.mark.parametrize("threads", ["1", "3"])
 def test_host_md5_pool_matches_plain_chain(threads):
-    """fg_md5_host.cpp's hashing pool (the file path's MD5 engine: up to four callers' chains
-    interleaved per worker) equals one plain chain per message, many callers at once, updates split
+    """fg_md5_host.cpp's hashing pool (the file path's MD5 engine: up to eight callers' chains
+    interleaved per worker; one worker holds all eight here) equals one plain chain per message, many callers at once, updates split
     at odd offsets (tests/cpp/md5_pool_test.cpp)."""
     import os
     import subprocess

@@ -83,3 +83,19 @@ def test_md5_many_no_pool_matches(monkeypatch):
     env = dict(os.environ, FLACGPU_MD5_THREADS="-1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
+def test_md5_many_more_chains_than_four_per_worker():
+    """40 pool-sized messages on 2 workers: each worker interleaves up to eight chains
+    (fg_md5_host.cpp kMaxChains), 5-8 at once as they finish; digests equal hashlib's.  In a child
+    so the pool's size is read afresh."""
+    _lib_or_skip()
+    import subprocess
+
+    code = ("import sys, hashlib; sys.path.insert(0, %r); import flacgpu;"
+            "c=[bytes([i, 255 - i]) * (40000 + 4160 * i) for i in range(40)];"
+            "assert flacgpu.md5_many(c) == [hashlib.md5(x).digest() for x in c]; print('ok')"
+            % os.path.join(os.path.dirname(__file__), "..", "zig-flac_amd"))
+    env = dict(os.environ, FLACGPU_MD5_THREADS="2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr

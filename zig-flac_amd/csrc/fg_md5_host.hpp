@@ -21,7 +21,7 @@ struct HostMd5 {
 };
 
 // h->update(data, len) on the process-wide hashing pool (fg_md5_host.cpp): the bulk of a long
-// update runs on a pool worker that hashes up to four callers' messages at once, their chains
+// update runs on a pool worker that hashes up to eight callers' messages at once, their chains
 // interleaved step by step (one MD5 chain leaves most of a core's ALU ports idle), so files
 // encoded concurrently hash 2-3x faster per core than one scalar chain each.  Blocks until done.
 // FLACGPU_MD5_THREADS sets the worker count (default: the process's CPU share -- the cgroup quota,
