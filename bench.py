@@ -618,7 +618,7 @@ def end_to_end(args):
                     "per_file = flacgpu_encode_file per file (one context + host thread each), batch = ONE "
                     "flacgpu_encode_files call on one context (one pipelined H2D / kernels / D2H schedule in "
                     "2048-frame chunks running on from file to file); every file's MD5 on the library's host "
-                    "hashing pool beside the encode (up to 4 chains interleaved per core, fg_md5_host.cpp)",
+                    "hashing pool beside the encode (up to 8 chains interleaved per core, fg_md5_host.cpp)",
             "md5_pool_threads": os.environ.get("FLACGPU_MD5_THREADS", "default (CPUs of the affinity mask)"),
             "output_ok": bool(ok)}
 
