@@ -7,6 +7,7 @@
 // GPU kernels via flacgpu_encode_frames; only the 73 metadata bytes are built
 // here.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <system_error>
 #include <thread>
@@ -205,7 +206,9 @@ int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sa
 // H2D / encode / D2H schedule (fg::ctx_encode_segments: the pipeline runs on from file to file;
 // one context's streams, not one context per file contending for the GPU's hardware queues),
 // and every file's MD5 on the host hashing pool in one batch beside it (md5_pool_update_many:
-// up to four chains per core).  Each out[i] receives exactly what flacgpu_encode_file writes.
+// up to eight chains per core).  Each out[i] receives exactly what flacgpu_encode_file writes.
+// FLACGPU_FILES_MD5=0 (diagnostic only: times the GPU / PCIe schedule alone) skips the hashing and
+// leaves the STREAMINFO MD5 zero, which FLAC defines as "not computed".
 int flacgpu_encode_files(flacgpu_ctx *ctx, uint32_t n_files, const void *const *pcm, uint32_t bytes_per_sample,
                          const uint64_t *n_samples, uint8_t *const *out, const size_t *out_cap, size_t *out_len) {
     if (!ctx || (n_files && (!pcm || !n_samples || !out || !out_cap || !out_len))) return FLACGPU_ERR_INVALID_INPUT;
@@ -248,9 +251,11 @@ int flacgpu_encode_files(flacgpu_ctx *ctx, uint32_t n_files, const void *const *
     } catch (...) {
         return FLACGPU_ERR_OUT_OF_MEMORY;
     }
-    const bool host_md5 = flacgpu_md5_get_engine(ctx) == FLACGPU_MD5_HOST;
+    const char *mk = std::getenv("FLACGPU_FILES_MD5");
+    const bool no_md5 = mk && mk[0] == '0';
+    const bool host_md5 = no_md5 || flacgpu_md5_get_engine(ctx) == FLACGPU_MD5_HOST;
     std::thread hasher;
-    if (host_md5) {
+    if (host_md5 && !no_md5) {
         try {
             hasher = std::thread([&]() { fg::md5_pool_update_many(hp.data(), src.data(), bytes.data(), n_files); });
         } catch (const std::system_error &) {
@@ -266,7 +271,9 @@ int flacgpu_encode_files(flacgpu_ctx *ctx, uint32_t n_files, const void *const *
         flacgpu_streaminfo_init(&si, cfg.sample_rate, cfg.channels, cfg.bits_per_sample, n_samples[i], cfg.block_size);
         const uint64_t nf = (n_samples[i] + cfg.block_size - 1) / cfg.block_size;
         for (uint64_t f = 0; f < nf; f++) flacgpu_streaminfo_update_frame_size(&si, sizes[i][f]);
-        if (host_md5) {
+        if (no_md5) {
+            memset(si.md5, 0, 16);
+        } else if (host_md5) {
             md5[i].final(si.md5);
         } else {
             if ((rc = flacgpu_md5_init(ctx)) || (rc = flacgpu_md5_update(ctx, pcm[i], bytes[i])) ||
