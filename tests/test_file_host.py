@@ -138,6 +138,22 @@ def test_gpu_encode_files_matches_oracle(ch, bits, rate, engine):
 
 
 @pytest.mark.gpu
+def test_gpu_encode_files_without_md5_diagnostic(monkeypatch):
+    """FLACGPU_FILES_MD5=0 (diagnostic: the schedule without its hashing) changes nothing but the
+    STREAMINFO MD5, written as zero ("not computed"; bytes 26..41 of the file)."""
+    ch, bits, rate = 2, 16, 44100
+    lens = [3 * 4096 + 1000, 0, 9 * 4096]
+    pcms = [synth.synth_pcm(n, ch, bits, rate, stream=60 + i) if n else b"" for i, n in enumerate(lens)]
+    monkeypatch.setenv("FLACGPU_FILES_MD5", "0")
+    with flacgpu.Encoder(ch, bits, rate, max_frames=8) as enc:
+        outs = enc.encode_files(pcms)
+    for i, pcm in enumerate(pcms):
+        ref = oracle_ref.encode_file(pcm, ch, bits, rate)
+        assert outs[i][:26] == ref[:26] and outs[i][42:] == ref[42:], f"file {i}"
+        assert outs[i][26:42] == bytes(16)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("block", [1152, 4096, 192, 4000])
 def test_gpu_encode_file_block_sizes(block):
     """STREAMINFO min/max block size follows the context's block size (the reference only
