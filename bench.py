@@ -885,6 +885,119 @@ def config_line(args, cfg, dist, rank, world, dev):
     return line
 
 
+# ---------------------------------------------------------------------------------------------
+# the stdout line: the driver keeps only the tail of stdout (about 8 KB), so the line it parses is a
+# compact summary of at most LINE_MAX bytes; the full record goes to a sidecar file (`detail`)
+LINE_MAX = 4096
+
+
+def _r(x, nd=4):
+    return round(x, nd) if isinstance(x, float) else x
+
+
+def _compact_roofline(r):
+    if not r:
+        return None
+    ks = {}
+    for k, v in (r.get("kernels") or {}).items():
+        ks[k] = {"ms": v.get("avg_launch_ms"), "frac": _r(v.get("frac")), "traffic_ratio": v.get("traffic_ratio"),
+                 "issue": (v.get("issue") or {}).get("valu_issue_frac")}
+    out = {"bound": r.get("bound"), "kernel": r.get("kernel"), "achieved": r.get("achieved"), "peak": r.get("peak"),
+           "unit": r.get("unit"), "frac": r.get("frac"), "traffic": r.get("traffic"),
+           "traffic_ratio": (r.get("kernels") or {}).get(_dom_name(r), {}).get("traffic_ratio"),
+           "algorithmic_bytes_per_launch": r.get("algorithmic_bytes_per_launch"),
+           "avg_launch_ms": r.get("avg_launch_ms"), "step_issue_frac": r.get("step_issue_frac"),
+           "kernels": ks}
+    if r.get("weighted_issue_frac") is not None:
+        out["weighted_issue_frac"] = r["weighted_issue_frac"]
+    return out
+
+
+def _dom_name(r):
+    kern = r.get("kernel") or ""
+    return "md5" if "md5" in kern else ("pack" if "pack" in kern and "analyze" not in kern else "analyze")
+
+
+def _compact_cpu(c):
+    if not c:
+        return None
+    return {"value": c.get("value"), "unit": c.get("unit"), "cores": c.get("cores"), "kind": c.get("kind"),
+            "sample": c.get("sample", "")[:120],
+            "single_core": (c.get("single_core") or {}).get("value"),
+            "single_socket_estimate": c.get("single_socket_estimate"),
+            "fixed_only": (c.get("fixed_only") or {}).get("value"), "cpu_model": c.get("cpu_model")}
+
+
+def compact_line(full: dict, detail_path: str | None = None) -> dict:
+    """The driver-parsed stdout line built from the full record: the contract keys, a compact
+    roofline and CPU baseline, one summary per BASELINE config and one-number summaries of the
+    stream curve, the end-to-end path and the sharded stream.  len(json.dumps(...)) <= LINE_MAX
+    (tests/test_bench_line.py); everything else is in the sidecar named by `detail`."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: full.get(k) for k in keep}
+    cfg = full.get("config") or {}
+    line["config"] = {"workload": cfg.get("workload_key"), "blocks_per_gpu_per_step": cfg.get("blocks_per_gpu_per_step"),
+                      "streams_per_gpu": cfg.get("streams_per_gpu"), "channels_bits_rate": cfg.get("channels_bits_rate"),
+                      "compression_ratio": cfg.get("compression_ratio"), "parallelism": cfg.get("parallelism")}
+    line["roofline"] = _compact_roofline(full.get("roofline"))
+    line["kernel_ms_per_step"] = full.get("kernel_ms_per_step")
+    line["output_ok"] = full.get("output_ok")
+    line["cpu_baseline"] = _compact_cpu(full.get("cpu_baseline"))
+    cs = {}
+    for c in full.get("configs") or []:
+        if not c:
+            continue
+        r = c.get("roofline") or {}
+        cb = c.get("cpu_baseline") or {}
+        cs[c["config"]] = {"value": c.get("value"), "ms_per_step": c.get("ms_per_step"),
+                           "kernel_ms": c.get("kernel_ms_per_step"), "frac": r.get("frac"),
+                           "step_issue_frac": r.get("step_issue_frac"),
+                           "traffic_ratio": (r.get("kernels") or {}).get(_dom_name(r), {}).get("traffic_ratio"),
+                           "output_ok": c.get("output_ok"), "cpu": cb.get("value"),
+                           "cpu_single_core": (cb.get("single_core") or {}).get("value")}
+    line["configs"] = cs or None
+    sc = full.get("stream_curve")
+    if sc:
+        line["stream_curve"] = {str(p["streams"]): [p.get("value"), p.get("md5_engine"),
+                                                    (p.get("other") or {}).get("value")] for p in sc}
+        line["stream_curve_ok"] = all(p.get("md5_ok") and (p.get("other") or {}).get("md5_ok", True) for p in sc)
+    e = full.get("end_to_end")
+    if e:
+        top = max(e.get("curve") or [{}], key=lambda c: c.get("files", 0))
+        line["end_to_end"] = {"value": e.get("value"), "files": e.get("files"), "mode": e.get("mode"),
+                              "batch_frac_of_md5_bound": {str(c["files"]): c["batch"]["frac_of_md5_bound"]
+                                                          for c in e.get("curve") or []},
+                              "batch_h2d_d2h_gbs": e.get("batch_gbs"),
+                              "largest_batch": (top.get("batch") or {}).get("value"),
+                              "vs_cpu_single_socket_estimate": e.get("vs_cpu_single_socket_estimate"),
+                              "output_ok": e.get("output_ok")}
+    s = full.get("sharded_stream")
+    if s:
+        line["sharded_stream"] = {"value": s.get("value"), "ranks": s.get("ranks"), "ms_per_window": s.get("ms_per_window"),
+                                  "output_ok": s.get("output_ok")}
+    line["detail"] = detail_path
+    # last resort, never expected: drop the largest optional blocks until the line fits
+    for k in ("stream_curve", "end_to_end", "kernel_ms_per_step", "configs"):
+        if len(json.dumps(line)) <= LINE_MAX:
+            break
+        line.pop(k, None)
+    return line
+
+
+def write_detail(full: dict) -> str | None:
+    """The full record as a sidecar JSON file (FLACGPU_BENCH_DETAIL, default gpurun_out/bench_detail.json
+    under the repo root); returns its path relative to the repo root, None if it cannot be written."""
+    path = os.environ.get("FLACGPU_BENCH_DETAIL") or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+        return os.path.relpath(path, ROOT)
+    except OSError:
+        return None
+
+
 def visible_gpus() -> int:
     """GPUs this process could use, counted in a child process: the launcher itself never loads
     torch or touches the GPU (FLACGPU_BENCH_FAKE_GPUS overrides the count: CPU tests)."""
@@ -1080,6 +1193,7 @@ def main():
                 "workload_key": key,
                 "blocks_per_gpu_per_step": args.frames,
                 "streams_per_gpu": args.streams,
+                "channels_bits_rate": f"{args.channels}ch/{args.bits}-bit/{args.rate}Hz",
                 "samples_per_gpu_per_step": samples_per_rank,
                 "compression_ratio": round(total_bytes / pcm_bytes, 4),
                 "parallelism": f"streams sharded over {world} GPU(s), no collective on the data path",
@@ -1095,8 +1209,10 @@ def main():
             "end_to_end": e2e,
             "cpu_baseline": cpu,
         }
+        detail = write_detail(line)
+        print("bench.py full record: " + json.dumps(line), file=sys.stderr)
         sys.stdout.flush()
-        os.write(json_fd, (json.dumps(line) + "\n").encode())
+        os.write(json_fd, (json.dumps(compact_line(line, detail)) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 

@@ -1,0 +1,60 @@
+"""bench.py's stdout line fits what the driver captures (the 20,659-byte r4 line
+was cut by the driver's ~8 KB stdout tail, so BENCH_r04 was never parsed).  CPU only."""
+import json
+import os
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONTRACT = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config")
+
+
+def _full():
+    return json.load(open(os.path.join(ROOT, "profiles", "r4z_bench.json")))
+
+
+def test_compact_line_fits_and_has_contract_keys():
+    full = _full()
+    line = bench.compact_line(full, "gpurun_out/bench_detail.json")
+    s = json.dumps(line)
+    assert len(s) <= bench.LINE_MAX
+    for k in CONTRACT:
+        assert k in line, k
+    assert line["value"] == full["value"] and line["ms_per_step"] == full["ms_per_step"]
+    assert line["metric"] == bench.METRIC
+    r = line["roofline"]
+    for k in ("bound", "kernel", "achieved", "peak", "frac", "traffic_ratio", "step_issue_frac"):
+        assert k in r, k
+    c = line["cpu_baseline"]
+    for k in ("value", "cores", "kind", "single_core", "single_socket_estimate", "cpu_model"):
+        assert k in c, k
+    assert set(line["configs"]) == {"c3", "c4", "c5"}
+    for v in line["configs"].values():
+        for k in ("value", "ms_per_step", "frac", "step_issue_frac", "output_ok"):
+            assert k in v
+    assert line["end_to_end"]["value"] == full["end_to_end"]["value"]
+    assert line["sharded_stream"]["value"] == full["sharded_stream"]["value"]
+
+
+def test_compact_line_survives_the_driver_tail():
+    """The line the driver sees is the last 8,392 characters of stdout: with rank 0's one line the
+    whole line is inside it and parses."""
+    s = json.dumps(bench.compact_line(_full(), "x")) + "\n"
+    tail = s[-8392:]
+    assert json.loads(tail.strip())["value"] > 0
+
+
+def test_compact_line_bounded_even_when_blocks_grow():
+    full = _full()
+    p0 = full["stream_curve"][1]
+    full["stream_curve"] = [dict(p0, streams=i + 1) for i in range(400)]  # absurdly many curve points
+    assert len(json.dumps(bench.compact_line(full, "x"))) <= bench.LINE_MAX
+
+
+def test_detail_sidecar_written(tmp_path, monkeypatch):
+    p = tmp_path / "d.json"
+    monkeypatch.setenv("FLACGPU_BENCH_DETAIL", str(p))
+    full = _full()
+    bench.write_detail(full)
+    assert json.load(open(p))["value"] == full["value"]
