@@ -80,6 +80,14 @@ void flacgpu_close(flacgpu_ctx *ctx);
 const char *flacgpu_strerror(int code);
 int flacgpu_abi_version(void);
 
+/* How this libflacgpu.so was built (no reference counterpart: library introspection).
+ * FLACGPU_BUILD_DIAG: a diagnostic build (`make diag`) with the measured-slower alternative
+ * kernels / schedules and the diagnostic environment knobs compiled in; the release build has
+ * none of them.  FLACGPU_BUILD_STAMPS: per-phase clock stamps (-DFG_STAMPS). */
+#define FLACGPU_BUILD_DIAG 1u
+#define FLACGPU_BUILD_STAMPS 2u
+uint32_t flacgpu_build_flags(void);
+
 /* maxFrameBytes (encoder.zig:583-595) of the reference, and the tight bound
  * the GPU path uses for its per-frame LDS image. */
 size_t flacgpu_reference_max_frame_bytes(const flacgpu_config *cfg);
@@ -236,9 +244,33 @@ int flacgpu_md5_many(uint32_t n, const void *const *data, const uint64_t *lens, 
  * instead of one GPU lane each. */
 int flacgpu_md5_plan_host(const flacgpu_plan *plan, const void *h_pcm, flacgpu_md5_state *states, uint8_t *digests);
 /* The faster MD5 engine for this plan's segments: FLACGPU_MD5_HOST below the
- * stream-count crossover (a few long chains), FLACGPU_MD5_DEVICE above it (the
- * model and its measured constants: DESIGN.md section 5.2). */
+ * stream-count crossover (a few long chains), FLACGPU_MD5_DEVICE above it:
+ * flacgpu_md5_engine_for(plan's stream count, longest segment, total bytes). */
 int flacgpu_plan_md5_engine(const flacgpu_plan *plan);
+
+/* The rates the engine choice is priced with (no reference
+ * counterpart: the reference hashes on its one thread).  host_chain[k - 1]: bytes/s
+ * per pool worker when every worker interleaves k chains (k = 1..4), MEASURED on
+ * this machine by running the pool the first time they are needed
+ * (flacgpu_md5_get_rates); host_workers: the pool's size (0: no pool, host_chain
+ * is one chain on the caller); device_lane / device_chip: bytes/s of one stream's
+ * GPU lane beside the encode and of all lanes together (MI355X measurements). */
+typedef struct {
+    double host_chain[4];
+    double device_lane;
+    double device_chip;
+    int32_t host_workers;
+    int32_t measured; /* 1: host_chain measured in this process; 2: set by the caller */
+} flacgpu_md5_rates;
+/* The current rates (measures the host ones on first use, ~2 ms).  Needs no GPU. */
+int flacgpu_md5_get_rates(flacgpu_md5_rates *out);
+/* Replace the rates (NULL: measure again); e.g. a caller's own measurement. */
+int flacgpu_md5_set_rates(const flacgpu_md5_rates *rates);
+/* The engine the rates predict faster for n_streams chains of at most max_len
+ * bytes, total_len bytes in all: host time = total / (pool throughput at
+ * ceil(n / workers) chains per worker, time-sliced past 4), device time =
+ * max(max_len / device_lane, total / device_chip).  Needs no GPU. */
+int flacgpu_md5_engine_for(uint32_t n_streams, uint64_t max_len, uint64_t total_len);
 
 /* Synchronise hip_stream (NULL: the context's stream) and report the device-side
  * error word of the kernels queued so far (FLACGPU_ERR_OUTPUT_TOO_SMALL when a
@@ -367,7 +399,9 @@ int flacgpu_set_records(flacgpu_ctx *ctx, int enable);
  * range i+1 beside the scan + pack of range i on a second HIP stream, the two persistent grids
  * capped at ana_per_cu / pack_per_cu workgroups per CU (0 = no cap); calls with fewer than
  * ranges * min_frames full frames use fewer ranges.  ranges <= 1: one analysis, scan and pack
- * launch per call.  Output bytes are the same either way. */
+ * launch per call.  Output bytes are the same either way.  The overlapped schedule measured
+ * slower than the serial one: ranges > 1 is FLACGPU_ERR_INVALID_CONFIG unless the library is a
+ * diagnostic build (flacgpu_build_flags() & FLACGPU_BUILD_DIAG). */
 int flacgpu_set_overlap(flacgpu_ctx *ctx, uint32_t ranges, uint32_t ana_per_cu, uint32_t pack_per_cu,
                         uint32_t min_frames);
 int flacgpu_get_records(flacgpu_ctx *ctx, flacgpu_frame_record *out, uint64_t max_frames, uint64_t *n_frames);

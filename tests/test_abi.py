@@ -102,3 +102,37 @@ def test_multi_rejects_bad_arguments():
     n = ctypes.c_size_t(0)
     assert lib.flacgpu_multi_encode_frames(None, None, 2, 0, 0, None, 0, ctypes.byref(n), None) == -2
     lib.flacgpu_close_multi(None)  # no-op
+
+
+def _kernel_symbols():
+    import subprocess
+
+    nm = "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not os.path.exists(nm):
+        nm = "nm"
+    out = subprocess.run([nm, "-C", flacgpu.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    return out
+
+
+@pytest.mark.skipif(os.environ.get("FLACGPU_LIB") is not None, reason="checks the in-tree release library")
+def test_release_library_has_no_diagnostic_kernels():
+    """the release libflacgpu.so carries neither the one-wave analysis (k_ana1)
+    nor the fused single-pass kernel (k_analyze<..., FP = true>); they live in `make diag` only."""
+    assert flacgpu.build_flags() & flacgpu.BUILD_DIAG == 0
+    syms = _kernel_symbols()
+    assert "k_analyze<2, 16, true, 256, 2, 0, false>" in syms  # the C2 analysis is there
+    assert "k_ana1" not in syms
+    assert "k_analyze<2, 16, true, 256, 2, 0, true>" not in syms
+
+
+@pytest.mark.skipif(os.environ.get("FLACGPU_LIB") is not None, reason="checks the in-tree release library")
+def test_release_library_ignores_diagnostic_knobs():
+    """FLACGPU_FILES_MD5=0 (and the other diagnostic knobs) exist only in diagnostic builds: the
+    release library's code never reads them, so a stray environment variable cannot make it
+    write a zero STREAMINFO MD5 (encoder.zig:168-170 always finalises it)."""
+    import subprocess
+
+    strings = subprocess.run(["strings", flacgpu.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    for knob in ("FLACGPU_FILES_MD5", "FLACGPU_FUSED", "FLACGPU_ANA1", "FLACGPU_OVERLAP", "FLACGPU_ENC_PRIO",
+                 "FLACGPU_MD5_RESERVE", "FLACGPU_SPIN_SYNC"):
+        assert knob not in strings, knob

@@ -139,18 +139,36 @@ def test_gpu_encode_files_matches_oracle(ch, bits, rate, engine):
 
 @pytest.mark.gpu
 def test_gpu_encode_files_without_md5_diagnostic(monkeypatch):
-    """FLACGPU_FILES_MD5=0 (diagnostic: the schedule without its hashing) changes nothing but the
-    STREAMINFO MD5, written as zero ("not computed"; bytes 26..41 of the file)."""
+    """FLACGPU_FILES_MD5=0 (diagnostic builds only: the schedule without its hashing) changes nothing
+    but the STREAMINFO MD5, written as zero ("not computed"; bytes 26..41 of the file).  The release
+    library ignores it: every file is byte-identical to the restatement's, MD5 included."""
     ch, bits, rate = 2, 16, 44100
     lens = [3 * 4096 + 1000, 0, 9 * 4096]
     pcms = [synth.synth_pcm(n, ch, bits, rate, stream=60 + i) if n else b"" for i, n in enumerate(lens)]
     monkeypatch.setenv("FLACGPU_FILES_MD5", "0")
     with flacgpu.Encoder(ch, bits, rate, max_frames=8) as enc:
         outs = enc.encode_files(pcms)
+    diag = flacgpu.diag_build()
     for i, pcm in enumerate(pcms):
         ref = oracle_ref.encode_file(pcm, ch, bits, rate)
         assert outs[i][:26] == ref[:26] and outs[i][42:] == ref[42:], f"file {i}"
-        assert outs[i][26:42] == bytes(16)
+        assert outs[i][26:42] == (bytes(16) if diag else ref[26:42])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["max_frames_1", "records_on"])
+def test_gpu_encode_files_where_the_pipeline_cannot_run(mode):
+    """flacgpu_encode_files on the contexts its pipelined schedule cannot serve (one frame per call;
+    decision records on) encodes file by file, as flacgpu_encode_file does."""
+    ch, bits, rate = 2, 16, 44100
+    lens = [2 * 4096 + 77, 0, 4096]
+    pcms = [synth.synth_pcm(n, ch, bits, rate, stream=70 + i) if n else b"" for i, n in enumerate(lens)]
+    with flacgpu.Encoder(ch, bits, rate, max_frames=1 if mode == "max_frames_1" else 8) as enc:
+        if mode == "records_on":
+            enc.set_records(True)
+        outs = enc.encode_files(pcms)
+    for i, pcm in enumerate(pcms):
+        assert outs[i] == oracle_ref.encode_file(pcm, ch, bits, rate), f"file {i}"
 
 
 @pytest.mark.gpu

@@ -23,6 +23,11 @@ pytestmark = pytest.mark.gpu
 CH, BITS, RATE = 2, 16, 44100
 
 
+@pytest.fixture(autouse=True)
+def _diag_only(diag_build):
+    """The fused kernel ships in diagnostic builds only."""
+
+
 @pytest.fixture
 def fused(monkeypatch):
     monkeypatch.setenv("FLACGPU_FUSED", "1")

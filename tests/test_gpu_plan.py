@@ -395,7 +395,7 @@ def test_md5_kernels_ragged(kernel, monkeypatch):
 @pytest.mark.parametrize("ch,bits,rate,lpc", [(2, 16, 44100, 0), (8, 24, 96000, 0), (2, 24, 96000, 8),
                                               (2, 32, 192000, 0), (1, 16, 48000, 0)])
 @pytest.mark.parametrize("ranges,ana,pack", [(4, 2, 2), (3, 0, 0), (7, 1, 3)])
-def test_overlapped_schedule_matches_oracle(ch, bits, rate, lpc, ranges, ana, pack):
+def test_overlapped_schedule_matches_oracle(ch, bits, rate, lpc, ranges, ana, pack, diag_build):
     fb = ch * (bits // 8)
     offs, size = _layout(LENGTHS, fb, (4, 8, 12, 0))
     buf = bytearray(size)
@@ -416,7 +416,7 @@ def test_overlapped_schedule_matches_oracle(ch, bits, rate, lpc, ranges, ana, pa
                     assert dig == ref_md5, f"stream {s}: MD5"
 
 
-def test_overlapped_schedule_many_ranges_and_serial_again():
+def test_overlapped_schedule_many_ranges_and_serial_again(diag_build):
     """64 ranges of a long plan, then the serial schedule on the same context (ticket sets shared)."""
     ch, bits, rate = 2, 16, 44100
     lengths = [4096 * 16 + 5] * 24 + [4096 * 7] * 8
@@ -434,6 +434,19 @@ def test_overlapped_schedule_many_ranges_and_serial_again():
             res, _ = _run_plan(enc, bytes(buf), offs, lengths, md5="none")
             for s, (got, sizes, _) in enumerate(res):
                 assert (got, sizes) == (refs[s][0], refs[s][1]), f"ranges {ranges} stream {s}"
+
+
+def test_overlap_refused_in_release_build():
+    """The release library refuses ranges > 1 (the schedule is a diagnostic-build alternative);
+    ranges <= 1 (the serial schedule) is accepted."""
+    import flacgpu
+
+    if flacgpu.diag_build():
+        pytest.skip("release build only")
+    with _encoder(2, 16, 44100) as enc:
+        enc.set_overlap(1, 2, 2)
+        with pytest.raises(flacgpu.FlacGpuError):
+            enc.set_overlap(4, 2, 2)
 
 
 def _host_replay(sizes, lo=0xFFFFFF, hi=0):
@@ -479,7 +492,7 @@ def test_streaminfo_replay_device_matches_host(n, shape, carried):
 
 
 @pytest.mark.parametrize("variant", ["1", "2"])
-def test_one_wave_analysis_matches_oracle(variant, monkeypatch):
+def test_one_wave_analysis_matches_oracle(variant, monkeypatch, diag_build):
     """k_ana1 (fg_ana1.hpp: one wave per full 16-bit stereo frame, FLACGPU_ANA1=1 / 2) writes the
     same frames and sizes as the restatement (and so as k_analyze), and the same decision records."""
     monkeypatch.setenv("FLACGPU_ANA1", variant)

@@ -86,9 +86,10 @@ def test_md5_many_no_pool_matches(monkeypatch):
 
 
 def test_md5_many_more_chains_than_four_per_worker():
-    """40 pool-sized messages on 2 workers: each worker interleaves up to eight chains
-    (fg_md5_host.cpp kMaxChains), 5-8 at once as they finish; digests equal hashlib's.  In a child
-    so the pool's size is read afresh."""
+    """40 pool-sized messages of different lengths on 2 workers: each worker interleaves up to four
+    chains (fg_md5_host.cpp kMaxChains) and, with chains waiting, yields them to the queue's tail
+    after every chunk (time slicing), so every chain passes between workers many times; digests
+    equal hashlib's.  In a child so the pool's size is read afresh."""
     _lib_or_skip()
     import subprocess
 
@@ -99,3 +100,51 @@ def test_md5_many_more_chains_than_four_per_worker():
     env = dict(os.environ, FLACGPU_MD5_THREADS="2")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
+def _rates(host, workers, lane=72e6, chip=600e9):
+    r = flacgpu.Md5Rates()
+    for i, v in enumerate(host):
+        r.host_chain[i] = v
+    r.device_lane, r.device_chip, r.host_workers = lane, chip, workers
+    return r
+
+
+def test_md5_engine_picker_with_injected_rates():
+    """flacgpu_md5_engine_for prices both engines with the rates it is given:
+    the host pool's time = total / (k-chain rate x workers) (k = chains per worker, at most 4), the
+    device's = max(longest chain / lane rate, total / chip rate).  CPU only."""
+    _lib_or_skip()
+    H, D = flacgpu.MD5_HOST, flacgpu.MD5_DEVICE
+    try:
+        flacgpu.set_md5_rates(_rates([1e9, 1.7e9, 2.2e9, 2.6e9], 16))
+        per = 16 << 20
+        # 8 long chains: host 8 workers x 1 GB/s (16 ms) vs one lane at 72 MB/s (233 ms)
+        assert flacgpu.md5_engine_for(8, per, 8 * per) == H
+        # 16384 chains of 256 KiB: host 4 GiB / (16 x 2.6 GB/s) = 103 ms; device max(3.6, 7.2) ms
+        assert flacgpu.md5_engine_for(16384, 256 << 10, 16384 * (256 << 10)) == D
+        # 256 chains of 16 MiB: host 4 GiB / 41.6 GB/s = 103 ms; device 233 ms -> host
+        assert flacgpu.md5_engine_for(256, per, 256 * per) == H
+        # ... but on a slow host (0.3 GB/s per chain) the device wins the same shape
+        flacgpu.set_md5_rates(_rates([0.3e9, 0.5e9, 0.65e9, 0.78e9], 16))
+        assert flacgpu.md5_engine_for(256, per, 256 * per) == D
+        # no pool: chain after chain on the caller
+        flacgpu.set_md5_rates(_rates([1e9, 1.7e9, 2.2e9, 2.6e9], 0))
+        assert flacgpu.md5_engine_for(64, per, 64 * per) == D  # 1.07 s vs 0.23 s
+        assert flacgpu.md5_engine_for(2, per, 2 * per) == H    # 34 ms vs 233 ms
+        got = flacgpu.md5_rates()
+        assert got.measured == 2 and got.host_workers == 0
+        with pytest.raises(flacgpu.FlacGpuError):
+            flacgpu.set_md5_rates(_rates([0.0, 1, 1, 1], 4))
+    finally:
+        flacgpu.set_md5_rates(None)  # measure again on next use
+
+
+def test_md5_rates_measured_on_first_use():
+    _lib_or_skip()
+    flacgpu.set_md5_rates(None)
+    r = flacgpu.md5_rates()
+    assert r.measured == 1
+    assert all(v > 1e7 for v in r.host_chain)  # any host hashes > 10 MB/s
+    assert r.host_chain[3] > r.host_chain[0]  # interleaving four chains beats one on a core
+    assert r.host_workers >= 0

@@ -593,6 +593,17 @@ const char *flacgpu_strerror(int code) {
 
 int flacgpu_abi_version(void) { return FLACGPU_ABI_VERSION; }
 
+uint32_t flacgpu_build_flags(void) {
+    uint32_t f = 0;
+#if FG_DIAG
+    f |= FLACGPU_BUILD_DIAG;
+#endif
+#ifdef FG_STAMPS
+    f |= FLACGPU_BUILD_STAMPS;
+#endif
+    return f;
+}
+
 int flacgpu_get_config(const flacgpu_ctx *c, flacgpu_config *out) {
     if (!c || !out) return FLACGPU_ERR_INVALID_INPUT;
     *out = c->cfg;
@@ -662,24 +673,28 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     // (4 workgroups per CU; 2 for 32-bit samples)
     const uint32_t pack_wgs = c->B == 4 ? 2u : 4u;
     c->pack_dbuf = pack_layout(c->C, c->B, c->image_bytes, true).total * pack_wgs <= 160u * 1024u;
-    if (const char *e = std::getenv("FLACGPU_PACK_DBUF")) c->pack_dbuf = c->pack_dbuf && e[0] == '1';  // tuning knob
+    // output-invariant tuning knobs (schedule / kernel-variant choices; every setting is
+    // parity-tested: tests/test_gpu_parity.py, test_gpu_plan.py; INTEGRATION.md lists them)
+    if (const char *e = std::getenv("FLACGPU_PACK_DBUF")) c->pack_dbuf = c->pack_dbuf && e[0] == '1';
     // 32-bit samples (c5): the 48-KiB three-chunk ring (kernel 2) -- same-box A/B r4m, 2 reps:
     // c5 24.19-24.25k -> 24.67-24.68k MS/s (MD5 10.1 -> 9.5 ms, analysis 8.84 -> 8.58 ms beside
     // it); c3 neutral, C2 -4 %, so the others keep kernel 1
     if (c->B == 4u) c->md5_kernel = 2;
-    if (const char *e = std::getenv("FLACGPU_MD5_KERNEL")) c->md5_kernel = std::atoi(e);  // A/B knob
-    if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);      // A/B knob
-    if (const char *e = std::getenv("FLACGPU_ENC_PRIO")) c->enc_prio = e[0] == '1' ? 1u : 0u;  // A/B knob
-    if (const char *e = std::getenv("FLACGPU_MD5_RESERVE")) c->md5_reserve = std::atoi(e);  // A/B knob
-    if (const char *e = std::getenv("FLACGPU_MD5_DIAG")) c->md5_prio |= std::atoi(e) << 8;  // diagnostics
-    // overlapped encode: ranges per call, workgroups per CU of the analysis / pack grids (A/B knobs)
+    if (const char *e = std::getenv("FLACGPU_MD5_KERNEL")) c->md5_kernel = std::atoi(e);
+    if (const char *e = std::getenv("FLACGPU_XCD_QUEUE")) c->xcd_queue = e[0] != '0';
+    if (const char *e = std::getenv("FLACGPU_PACK_XCDQ")) c->pack_xcdq = e[0] != '0';
+    if (const char *e = std::getenv("FLACGPU_SPLIT_JIT")) c->split_jit = (uint32_t)std::atoi(e) & 3u;
+#if FG_DIAG
+    // diagnostic build only: issue priorities, grid reserves, the overlapped schedule's shape
+    if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);
+    if (const char *e = std::getenv("FLACGPU_ENC_PRIO")) c->enc_prio = e[0] == '1' ? 1u : 0u;
+    if (const char *e = std::getenv("FLACGPU_MD5_RESERVE")) c->md5_reserve = std::atoi(e);
+    if (const char *e = std::getenv("FLACGPU_MD5_DIAG")) c->md5_prio |= std::atoi(e) << 8;
     if (const char *e = std::getenv("FLACGPU_OVERLAP")) c->ovl_chunks = (uint32_t)std::atoi(e);
-    if (const char *e = std::getenv("FLACGPU_XCD_QUEUE")) c->xcd_queue = e[0] != '0';  // A/B knob
-    if (const char *e = std::getenv("FLACGPU_PACK_XCDQ")) c->pack_xcdq = e[0] != '0';   // A/B knob
-    if (const char *e = std::getenv("FLACGPU_SPLIT_JIT")) c->split_jit = (uint32_t)std::atoi(e) & 3u;  // A/B knob
     if (const char *e = std::getenv("FLACGPU_OVL_ANA")) c->ovl_ana = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_OVL_PACK")) c->ovl_pack = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_OVL_MIN")) c->ovl_min_frames = (uint32_t)std::max(1, std::atoi(e));
+#endif
     c->lds_pack = pack_layout(c->C, c->B, c->image_bytes, c->pack_dbuf).total;
     // CRC fold: half-segments of H words (odd), H <= ceil(image words / (2 * pack threads))
     c->crc_hmax = ((c->image_bytes / 4u + 2u * c->nt_pack - 1u) / (2u * c->nt_pack)) | 1u;
@@ -725,6 +740,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
             c->crc_hmaxs = ((img / 4u + 2u * c->nt_psplit - 1u) / (2u * c->nt_psplit)) | 1u;
         }
     }
+#if FG_DIAG
     if (c->C == 2 && c->B == 2 && !lpc && c->stereo) {
         c->ana1 = false;  // measured slower than k_analyze so far: opt-in
         if (const char *e = std::getenv("FLACGPU_ANA1")) {  // A/B knob: 0 = k_analyze, 1 / 2 = k_ana1 variant
@@ -736,6 +752,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         c->lds_fused = ana_layout(2, 2, 4, true, false, false, c->image_bytes).total;
         c->crc_hmaxf = ((c->image_bytes / 4u + 2u * 256u - 1u) / (2u * 256u)) | 1u;
     }
+#endif
     if (c->lds > 160u * 1024u || c->lds_tail > 160u * 1024u || c->lds_pack > 160u * 1024u ||
         c->lds_pack4 > 160u * 1024u) {
         delete c;
@@ -756,8 +773,10 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     if (hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     {
-        const char *e = std::getenv("FLACGPU_SPIN_SYNC");
-        const unsigned fl = hipEventDisableTiming | ((e && e[0] == '1') ? 0u : hipEventBlockingSync);
+        unsigned fl = hipEventDisableTiming | hipEventBlockingSync;
+#if FG_DIAG
+        if (const char *e = std::getenv("FLACGPU_SPIN_SYNC")) fl = e[0] == '1' ? hipEventDisableTiming : fl;
+#endif
         for (hipEvent_t &ev : c->hw)
             if (hipEventCreateWithFlags(&ev, fl) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     }
@@ -871,6 +890,9 @@ struct PipeSeg {
     uint32_t *frame_bytes;  // may be NULL
 };
 
+// encode_pipelined could not start its download thread: nothing was queued, encode sequentially
+constexpr int kNoWorker = -1000;
+
 static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     const uint32_t bs = c->cfg.block_size;
     const uint64_t stride = (uint64_t)bs * c->C * c->B;
@@ -934,7 +956,7 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     try {
         worker = std::thread(work);
     } catch (const std::system_error &) {
-        return FLACGPU_ERR_OUT_OF_MEMORY;
+        return kNoWorker;  // the caller encodes chunk by chunk on this thread instead
     }
     // wait (host) until at least `k` downloads have finished; the first download error
     auto wait_done = [&](uint64_t k) -> int {
@@ -1006,8 +1028,23 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
 
 int fg::ctx_encode_segments(flacgpu_ctx *c, uint32_t n, const uint8_t *const *src, const uint64_t *n_samples,
                             uint8_t *const *out, const size_t *out_cap, size_t *out_len, uint32_t *const *frame_bytes) {
-    if (c->max_frames < 2 || c->records_on) return FLACGPU_ERR_INVALID_CONFIG;
     HIPCHK(hipSetDevice(c->device));
+    // contexts the pipeline cannot serve (one frame per call, decision records on), or no thread
+    // for its downloads: each file through flacgpu_encode_frames, which is what
+    // flacgpu_encode_file does for them
+    auto one_by_one = [&]() -> int {
+        for (uint32_t i = 0; i < n; i++) out_len[i] = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const int r = flacgpu_encode_frames(c, src[i], c->B, n_samples[i], 0, out[i], out_cap[i], &out_len[i],
+                                                frame_bytes ? frame_bytes[i] : nullptr);
+            if (r) {
+                for (uint32_t j = 0; j < n; j++) out_len[j] = 0;
+                return r;
+            }
+        }
+        return FLACGPU_OK;
+    };
+    if (c->max_frames < 2 || c->records_on) return one_by_one();
     std::vector<PipeSeg> segs;
     try {
         segs.resize(n);
@@ -1020,6 +1057,7 @@ int fg::ctx_encode_segments(flacgpu_ctx *c, uint32_t n, const uint8_t *const *sr
         segs[i] = PipeSeg{src[i], n_samples[i], 0, out[i], out_cap[i], 0, frame_bytes ? frame_bytes[i] : nullptr};
     }
     const int rc = encode_pipelined(c, segs.data(), n);
+    if (rc == kNoWorker) return one_by_one();
     resolve_timing(c);
     for (uint32_t i = 0; i < n; i++) out_len[i] = rc ? 0 : segs[i].written;
     return rc;
@@ -1047,9 +1085,11 @@ int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sa
     if (!c->records_on && c->max_frames >= 2 && total_frames > std::min<uint64_t>(c->max_frames / 2u, 2048u)) {
         PipeSeg seg{src, n_samples, first_frame_number, out, out_cap, 0, frame_bytes};
         const int rc = encode_pipelined(c, &seg, 1);
-        resolve_timing(c);
-        if (rc == FLACGPU_OK) *out_len = seg.written;
-        return rc;
+        if (rc != kNoWorker) {
+            resolve_timing(c);
+            if (rc == FLACGPU_OK) *out_len = seg.written;
+            return rc;
+        }
     }
     (void)stride;
     while (frame0 < total_frames) {
@@ -1272,21 +1312,72 @@ int flacgpu_md5_plan_host(const flacgpu_plan *p, const void *h_pcm, flacgpu_md5_
                             p->h_md5_fin.empty() ? nullptr : p->h_md5_fin.data(), states, digests);
 }
 
+// The engine rates: device figures from bench.py's stream_curve on MI355X (DESIGN.md section 5.2:
+// one lane per stream at ~72 MB/s beside the encode, at most ~600 GB/s over the chip -- 16384
+// streams: 4.3 GB of MD5 in 7.1 ms); host figures measured on this machine the first time the
+// choice is made (fg::md5_measure_rates: the fixed 0.95 GB/s-per-chain constants of round 4 were
+// 1.6-3x off on the driver's box, where the picker then chose the slower engine).
+static std::mutex g_rates_mu;
+static flacgpu_md5_rates g_rates{};
+static bool g_rates_set = false;
+
+static flacgpu_md5_rates md5_rates() {
+    std::lock_guard<std::mutex> lk(g_rates_mu);
+    if (!g_rates_set) {
+        flacgpu_md5_rates r{};
+        fg::md5_measure_rates(r.host_chain);
+        r.device_lane = 72e6;
+        r.device_chip = 600e9;
+        r.host_workers = fg::md5_pool_workers();
+        r.measured = 1;
+        g_rates = r;
+        g_rates_set = true;
+    }
+    return g_rates;
+}
+
+int flacgpu_md5_get_rates(flacgpu_md5_rates *out) {
+    if (!out) return FLACGPU_ERR_INVALID_INPUT;
+    *out = md5_rates();
+    return FLACGPU_OK;
+}
+
+int flacgpu_md5_set_rates(const flacgpu_md5_rates *r) {
+    if (r) {
+        for (double v : r->host_chain)
+            if (!(v > 0)) return FLACGPU_ERR_INVALID_INPUT;
+        if (!(r->device_lane > 0) || !(r->device_chip > 0) || r->host_workers < 0) return FLACGPU_ERR_INVALID_INPUT;
+    }
+    std::lock_guard<std::mutex> lk(g_rates_mu);
+    if (r) {
+        g_rates = *r;
+        g_rates.measured = 2;
+    }
+    g_rates_set = r != nullptr;
+    return FLACGPU_OK;
+}
+
+int flacgpu_md5_engine_for(uint32_t n_streams, uint64_t max_len, uint64_t total_len) {
+    if (!n_streams || !total_len) return FLACGPU_MD5_DEVICE;
+    const flacgpu_md5_rates r = md5_rates();
+    const double n = n_streams;
+    const double t_dev = std::max((double)max_len / r.device_lane, (double)total_len / r.device_chip);
+    double t_host;
+    if (r.host_workers <= 0) {
+        t_host = (double)total_len / r.host_chain[0];  // no pool: the caller hashes chain after chain
+    } else {
+        // k chains per worker (time-sliced past four: the pool's throughput stays at k = 4); with
+        // fewer chains than workers, one chain each on n workers
+        const double w = r.host_workers;
+        const int k = (int)std::min(4.0, std::ceil(n / w));
+        t_host = std::max((double)total_len / (r.host_chain[k - 1] * std::min(n, w)), (double)max_len / r.host_chain[0]);
+    }
+    return t_host < t_dev ? FLACGPU_MD5_HOST : FLACGPU_MD5_DEVICE;
+}
+
 int flacgpu_plan_md5_engine(const flacgpu_plan *p) {
     if (!p || !p->n_streams) return FLACGPU_MD5_DEVICE;
-    // Time of each engine for the plan's segments, from the rates bench.py's stream_curve measured
-    // on MI355X: device -- one lane per stream at ~72 MB/s beside the encode,
-    // at most ~600 GB/s over the chip (16384 streams: 4.3 GB of MD5 in 7.1 ms); host -- the pool's
-    // workers at ~0.95 GB/s a chain, k chains interleaved on a worker (k <= 4) running k / g(k)
-    // times as long as one, g = 1, 1.7, 2.2, 2.6 (64 streams on 16 workers: 41 GB/s).
-    static const double g[5] = {1.0, 1.0, 1.7, 2.2, 2.6};
-    const double workers = std::max(1, fg::md5_pool_workers());
-    const double n = p->n_streams;
-    const double t_dev = std::max((double)p->md5_max_len / 72e6, (double)p->md5_total / 600e9);
-    const int k = (int)std::min(4.0, std::ceil(n / workers));
-    const double host_rate = 0.95e9 * std::min(n, workers) * g[k];
-    const double t_host = (double)p->md5_total / host_rate;
-    return t_host < t_dev ? FLACGPU_MD5_HOST : FLACGPU_MD5_DEVICE;
+    return flacgpu_md5_engine_for(p->n_streams, p->md5_max_len, p->md5_total);
 }
 
 // ---- plans (device-resident batches of independent streams) --------------
@@ -1514,6 +1605,8 @@ int flacgpu_reset_timing(flacgpu_ctx *c) {
 int flacgpu_set_overlap(flacgpu_ctx *c, uint32_t ranges, uint32_t ana_per_cu, uint32_t pack_per_cu,
                         uint32_t min_frames) {
     if (!c || ranges > kOvlMaxChunks || min_frames == 0) return FLACGPU_ERR_INVALID_INPUT;
+    // the overlapped schedule measured slower: diagnostic builds only
+    if (!FG_DIAG && ranges > 1) return FLACGPU_ERR_INVALID_CONFIG;
     c->ovl_chunks = ranges;
     c->ovl_ana = ana_per_cu;
     c->ovl_pack = pack_per_cu;

@@ -4,6 +4,14 @@
 #pragma once
 #include <stdint.h>
 
+// FG_DIAG=1 (`make diag`, build_diag/): the measured-slower alternatives (the one-wave analysis
+// k_ana1, the fused single-pass kernel, the overlapped schedule) and the diagnostic environment
+// knobs that can change what a call does (FLACGPU_FILES_MD5, issue priorities, grid reserves).
+// The release library (FG_DIAG=0, the default) compiles none of them.
+#ifndef FG_DIAG
+#define FG_DIAG 0
+#endif
+
 namespace fg {
 
 constexpr int kBlock = 4096;       // Config.default block size (encoder.zig:644)

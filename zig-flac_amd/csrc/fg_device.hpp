@@ -2631,7 +2631,9 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
 
 #include "fg_pack4.hpp"
 #include "fg_packw.hpp"
+#if FG_DIAG
 #include "fg_ana1.hpp"
+#endif
 
 // persistent launch: grid = min(work items, resident workgroups on this device).  The occupancy
 // is cached per (kernel, threads, LDS, device); the lock covers only the cache lookup/insert, so
@@ -2702,6 +2704,7 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
         // full 16-bit two-channel frames: four waves per written subframe (fg_pack4.hpp)
         if (stage == 1 && full && a.channels == 2 && threads == 512u)
             return launch_persistent(k_pack4<512>, a, threads, lds, st);
+#if FG_DIAG
         // fused single-pass encode of full 16-bit stereo frames (fg_fused.hpp)
         if (stage == 2 && full && a.channels == 2 && a.stereo && threads == 256u)
             return launch_persistent(k_analyze<2, 16, true, 256, 2, 0, true>, a, threads, lds, st);
@@ -2709,6 +2712,7 @@ static hipError_t launch_stage_b(int stage, const EncodeArgs &a, bool full, uint
         if (stage == 3 && full && a.channels == 2 && a.stereo && threads == 64u)
             return a.ana1_variant == 2 ? launch_persistent(k_ana1<2>, a, threads, lds, st)
                                        : launch_persistent(k_ana1<1>, a, threads, lds, st);
+#endif
     }
     if (stage >= 2) return hipErrorInvalidValue;
     // other full frames: WPS waves per written subframe (fg_packw.hpp); the host marks it by

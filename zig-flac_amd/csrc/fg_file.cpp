@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/flacgpu.h"
+#include "fg_common.hpp"
 #include "fg_internal.hpp"
 #include "fg_md5_host.hpp"
 
@@ -207,8 +208,9 @@ int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sa
 // one context's streams, not one context per file contending for the GPU's hardware queues),
 // and every file's MD5 on the host hashing pool in one batch beside it (md5_pool_update_many:
 // up to eight chains per core).  Each out[i] receives exactly what flacgpu_encode_file writes.
-// FLACGPU_FILES_MD5=0 (diagnostic only: times the GPU / PCIe schedule alone) skips the hashing and
-// leaves the STREAMINFO MD5 zero, which FLAC defines as "not computed".
+// Diagnostic builds only (FG_DIAG, `make diag`): FLACGPU_FILES_MD5=0 times the GPU / PCIe schedule
+// alone, skipping the hashing and leaving the STREAMINFO MD5 zero ("not computed").  The release
+// library always finalises the MD5 into STREAMINFO (encoder.zig:168-170).
 int flacgpu_encode_files(flacgpu_ctx *ctx, uint32_t n_files, const void *const *pcm, uint32_t bytes_per_sample,
                          const uint64_t *n_samples, uint8_t *const *out, const size_t *out_cap, size_t *out_len) {
     if (!ctx || (n_files && (!pcm || !n_samples || !out || !out_cap || !out_len))) return FLACGPU_ERR_INVALID_INPUT;
@@ -251,8 +253,12 @@ int flacgpu_encode_files(flacgpu_ctx *ctx, uint32_t n_files, const void *const *
     } catch (...) {
         return FLACGPU_ERR_OUT_OF_MEMORY;
     }
+#if FG_DIAG
     const char *mk = std::getenv("FLACGPU_FILES_MD5");
     const bool no_md5 = mk && mk[0] == '0';
+#else
+    const bool no_md5 = false;
+#endif
     const bool host_md5 = no_md5 || flacgpu_md5_get_engine(ctx) == FLACGPU_MD5_HOST;
     std::thread hasher;
     if (host_md5 && !no_md5) {

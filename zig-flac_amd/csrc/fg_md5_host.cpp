@@ -8,6 +8,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -241,11 +242,13 @@ class Md5Pool {
     int workers() const { return workers_; }
 
   private:
-    // up to eight chains per worker: more messages than 4 x workers then run as one round of 5-8
-    // chains on some workers (a core's throughput is flat past ~4 chains) instead of a second
-    // round that starts when the first ends (MD5 of 64 files on 15 workers 274-306 -> 212-214 ms, of
-    // 72 files on 16 workers 308 -> 212-218 ms: r4ze)
-    static constexpr int kMaxChains = 8;
+    // up to four chains interleaved per worker: a core's throughput is flat past ~4 chains and
+    // falls at 8 (the interleaved states no longer fit the x86-64 registers: 8 workers x 8 chains
+    // 3.4 GB/s, x 4 chains 4.5 GB/s, tools/md5_pool_rate.py).  More chains than 4 x workers are
+    // time-sliced: a worker that finishes a chunk while chains wait puts its own back at the
+    // queue's tail, so every chain advances in turn and the batch ends as one round, not with a
+    // tail round of the last few chains (r4ze measured that tail: 64 files on 15 workers)
+    static constexpr int kMaxChains = 4;
     static constexpr size_t kChunk = 256;  // blocks per chain between queue checks
     // The process's CPU share: the cgroup v2 quota where one is set (it is not visible in the
     // affinity mask), else the affinity mask.  Not OMP_NUM_THREADS: launchers such as torchrun
@@ -263,7 +266,14 @@ class Md5Pool {
         }
         cpu_set_t set;
         const int aff = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
-        return (n > 0 && n < aff) ? n : aff;
+        n = (n > 0 && n < aff) ? n : aff;
+        // one process per GPU (torchrun sets LOCAL_WORLD_SIZE): the node's ranks share the CPUs,
+        // so each rank's pool takes its share, not the whole mask
+        if (const char *e = std::getenv("LOCAL_WORLD_SIZE")) {
+            const int lw = std::atoi(e);
+            if (lw > 1) n = std::max(1, n / lw);
+        }
+        return n;
     }
     Md5Pool() : owner_(getpid()) {
         int n = 0;
@@ -314,11 +324,7 @@ class Md5Pool {
             case 1: compress_n<1>(st, bp, nb); break;
             case 2: compress_n<2>(st, bp, nb); break;
             case 3: compress_n<3>(st, bp, nb); break;
-            case 4: compress_n<4>(st, bp, nb); break;
-            case 5: compress_n<5>(st, bp, nb); break;
-            case 6: compress_n<6>(st, bp, nb); break;
-            case 7: compress_n<7>(st, bp, nb); break;
-            default: compress_n<8>(st, bp, nb); break;
+            default: compress_n<4>(st, bp, nb); break;
             }
             bool finished = false;
             for (auto *j : act) {
@@ -336,6 +342,15 @@ class Md5Pool {
                     }
                 done_cv_.notify_all();
                 act.erase(std::remove_if(act.begin(), act.end(), [](Md5Job *j) { return j->done; }), act.end());
+            }
+            if (!act.empty()) {
+                // chains waiting for a worker: yield this worker's to the queue's tail (time slicing)
+                std::lock_guard<std::mutex> lk(m_);
+                if (!q_.empty()) {
+                    for (auto *j : act) q_.push_back(j);
+                    active_ -= act.size();
+                    act.clear();
+                }
             }
         }
     }
@@ -356,6 +371,47 @@ void md5_pool_update_many(HostMd5 *const *hs, const uint8_t *const *data, const 
 }
 
 int md5_pool_workers() { return Md5Pool::get().workers(); }
+
+// Host MD5 rates on this machine: rate[k - 1] = bytes/s per pool worker with k chains each
+// (k = 1..4), measured by running the pool itself on k x workers chains of 256 KiB (one buffer
+// that stays in the caches: the pool's chains stream from memory, but MD5 at ~1 GB/s per chain is
+// far below what a core can fetch), so SMT siblings, the workers' placement and wake-up costs are
+// in the figure; best of three per k, ~3-8 ms in all.  Without a pool: one chain on the caller.
+void md5_measure_rates(double rate[4]) {
+    constexpr size_t kLen = 256 * 1024;
+    static uint8_t *buf = [] {
+        uint8_t *b = new uint8_t[kLen];
+        uint32_t x = 0x12345678u;
+        for (size_t i = 0; i < kLen; i++) {
+            x = x * 1664525u + 1013904223u;
+            b[i] = (uint8_t)(x >> 24);
+        }
+        return b;
+    }();
+    Md5Pool &pool = Md5Pool::get();
+    const int W = pool.workers();
+    for (int k = 1; k <= 4; k++) {
+        const size_t n = W > 0 ? (size_t)k * W : 1;
+        std::vector<HostMd5> hs(n);
+        std::vector<HostMd5 *> hp(n);
+        std::vector<const uint8_t *> ps(n, buf);
+        std::vector<size_t> lens(n, kLen);
+        for (size_t i = 0; i < n; i++) hp[i] = &hs[i];
+        double best = 0;
+        for (int rep = 0; rep < 3; rep++) {
+            const auto t0 = std::chrono::steady_clock::now();
+            if (W > 0) pool.run_many(hp.data(), ps.data(), lens.data(), n);
+            else hs[0].update(buf, kLen);
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (dt > 0) best = std::max(best, (double)n * kLen / dt / (W > 0 ? W : 1));
+        }
+        rate[k - 1] = best;
+        if (W == 0) {
+            for (int j = 1; j < 4; j++) rate[j] = best;
+            break;
+        }
+    }
+}
 
 void HostMd5::reset() {
     h[0] = 0x67452301u;

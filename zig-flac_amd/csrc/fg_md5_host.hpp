@@ -21,11 +21,13 @@ struct HostMd5 {
 };
 
 // h->update(data, len) on the process-wide hashing pool (fg_md5_host.cpp): the bulk of a long
-// update runs on a pool worker that hashes up to eight callers' messages at once, their chains
+// update runs on a pool worker that hashes up to four callers' messages at once, their chains
 // interleaved step by step (one MD5 chain leaves most of a core's ALU ports idle), so files
-// encoded concurrently hash 2-3x faster per core than one scalar chain each.  Blocks until done.
+// encoded concurrently hash 2-3x faster per core than one scalar chain each; more chains than
+// 4 x workers are time-sliced.  Blocks until done.
 // FLACGPU_MD5_THREADS sets the worker count (default: the process's CPU share -- the cgroup quota,
-// else the affinity mask's CPUs; -1: no pool, each caller hashes its own chain).
+// else the affinity mask's CPUs, divided by LOCAL_WORLD_SIZE when a launcher sets it; -1: no
+// pool, each caller hashes its own chain).
 void md5_pool_update(HostMd5 *h, const void *data, size_t len);
 
 // hs[i]->update(data[i], lens[i]) for n independent chains on the pool, queued together (the
@@ -34,5 +36,9 @@ void md5_pool_update_many(HostMd5 *const *hs, const uint8_t *const *data, const 
 
 // the pool's worker count (0: every caller hashes its own chain)
 int md5_pool_workers();
+
+// measured host MD5 rates: bytes/s per pool worker with k = 1..4 chains each, rate[k - 1]
+// (no pool: one chain's rate on the caller in every entry)
+void md5_measure_rates(double rate[4]);
 
 }  // namespace fg

@@ -118,6 +118,30 @@ def md5_many(chunks: Sequence, final: Optional[Sequence[bool]] = None, states=No
     return [raw[16 * i:16 * i + 16] if final is None or final[i] else None for i in range(n)]
 
 
+class Md5Rates(ctypes.Structure):
+    """flacgpu_md5_rates: the rates the MD5 engine choice is priced with (bytes/s)."""
+    _fields_ = [("host_chain", ctypes.c_double * 4), ("device_lane", ctypes.c_double),
+                ("device_chip", ctypes.c_double), ("host_workers", ctypes.c_int32), ("measured", ctypes.c_int32)]
+
+    def as_dict(self) -> dict:
+        return {"host_chain": list(self.host_chain), "device_lane": self.device_lane, "device_chip": self.device_chip,
+                "host_workers": self.host_workers, "measured": self.measured}
+
+
+def md5_rates() -> Md5Rates:
+    r = Md5Rates()
+    _check(load_library().flacgpu_md5_get_rates(ctypes.byref(r)), "md5_get_rates")
+    return r
+
+
+def set_md5_rates(r: Optional[Md5Rates]) -> None:
+    _check(load_library().flacgpu_md5_set_rates(ctypes.byref(r) if r is not None else None), "md5_set_rates")
+
+
+def md5_engine_for(n_streams: int, max_len: int, total_len: int) -> int:
+    return int(load_library().flacgpu_md5_engine_for(n_streams, max_len, total_len))
+
+
 class WavInfo(ctypes.Structure):
     """flacgpu_wav_info: WavReader's view of a WAV header (wav_reader.zig:116-170)."""
     _fields_ = [("sample_rate", ctypes.c_uint32), ("channels", ctypes.c_uint16), ("bits_per_sample", ctypes.c_uint16),
@@ -204,6 +228,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_close": (None, [P]),
         "flacgpu_strerror": (ctypes.c_char_p, [I32]),
         "flacgpu_abi_version": (I32, []),
+        "flacgpu_build_flags": (U32, []),
+        "flacgpu_md5_get_rates": (I32, [P]),
+        "flacgpu_md5_set_rates": (I32, [P]),
+        "flacgpu_md5_engine_for": (I32, [U32, U64, U64]),
         "flacgpu_reference_max_frame_bytes": (SZ, [ctypes.POINTER(Config)]),
         "flacgpu_frame_bound_bytes": (SZ, [ctypes.POINTER(Config)]),
         "flacgpu_encode_frames": (I32, [P, P, U32, U64, U64, P, SZ, ctypes.POINTER(SZ), P]),
@@ -265,6 +293,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 def exported_symbols() -> list:
     return [
         "flacgpu_config_default", "flacgpu_open", "flacgpu_close", "flacgpu_strerror", "flacgpu_abi_version",
+        "flacgpu_build_flags", "flacgpu_md5_get_rates", "flacgpu_md5_set_rates", "flacgpu_md5_engine_for",
         "flacgpu_reference_max_frame_bytes", "flacgpu_frame_bound_bytes", "flacgpu_encode_frames",
         "flacgpu_encode_frame_planar", "flacgpu_md5_init", "flacgpu_md5_update", "flacgpu_md5_final",
         "flacgpu_plan_create", "flacgpu_plan_destroy", "flacgpu_plan_frames", "flacgpu_plan_out_bound",
@@ -279,6 +308,20 @@ def exported_symbols() -> list:
         "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file", "flacgpu_encode_files",
         "flacgpu_wav_to_flac", "flacgpu_open_multi", "flacgpu_close_multi", "flacgpu_multi_encode_frames",
     ]
+
+
+BUILD_DIAG = 1  # FLACGPU_BUILD_DIAG
+BUILD_STAMPS = 2  # FLACGPU_BUILD_STAMPS
+
+
+def build_flags() -> int:
+    """flacgpu_build_flags(): BUILD_DIAG for a diagnostic build (`make diag`), else 0."""
+    L = load_library()
+    return int(L.flacgpu_build_flags()) if hasattr(L, "flacgpu_build_flags") else BUILD_DIAG
+
+
+def diag_build() -> bool:
+    return bool(build_flags() & BUILD_DIAG)
 
 
 STREAM_LEGACY = 1  # FLACGPU_STREAM_LEGACY: the library maps it to the HIP null stream
