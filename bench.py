@@ -1149,10 +1149,11 @@ def main():
         d_pcm = torch.from_numpy(buf).to(dev) if (rank == 0 and world == 1 and not args.no_curve
                                                   and not args.no_md5) else None
 
-    curve = e2e = cpu = None
+    curve = e2e = cpu = md5_rates = None
     if rank == 0 and world == 1:
         if not args.no_curve and not args.no_md5:
             curve = stream_curve(args, enc, d_pcm, buf, fb, dev)
+            md5_rates = flacgpu.md5_rates().as_dict()
         if not args.no_e2e and (args.config or "c2") == "c2":
             del d_pcm
             torch.cuda.empty_cache()
@@ -1205,6 +1206,7 @@ def main():
             "verified": vinfo,
             "configs": configs,
             "stream_curve": curve,
+            "md5_rates": md5_rates,
             "sharded_stream": sharded,
             "end_to_end": e2e,
             "cpu_baseline": cpu,
