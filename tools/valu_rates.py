@@ -1,14 +1,16 @@
 """Issue-slot estimate of a kernel's static VALU mix (hipcc -S listing), using the per-opcode rates
 measured on gfx950 by tools/micro/issue_micro.hip (wave64 instructions per SIMD-cycle, 8 waves per
-SIMD): full rate ~0.44 (v_add/sub/xor/or/shifts: 1 slot), half rate ~0.24 (VOP3 integer ops,
-v_max/min, mul24, mul_lo, bfe, cmp, DPP, SDWA, add3, lshl_or: 2 slots); ffbh ~quarter.
+SIMD; profiles/r5_issue_micro.txt): full rate ~0.44 (v_add/sub/xor/or/shifts: 1 slot), half rate
+~0.23 (VOP3 integer ops, v_max/min, mul24, mul_lo, bfe, cmp, cndmask, DPP, SDWA, add3, lshl_or,
+alignbit, mul_hi, v_mad_i64_i32 / v_mad_u64_u32, f64 fma/mul/add: 2 slots); ffbh ~quarter.
+(Round 4's cndmask figure, 0.061, read an uninitialised vcc: with an SGPR-pair mask it is 0.23.)
 Usage: python tools/valu_rates.py file.s symbol_substring"""
 import re
 import sys
 from collections import Counter
 
 FULL = re.compile(r"^v_(add|sub|subrev|xor|or|and|lshlrev|lshrrev|ashrrev|mov|not)_(u32|b32|i32|co_u32)(_e32|_e64)?$")
-QUARTER = re.compile(r"^v_(ffbh|ffbl|bcnt|mul_hi|mad_u64|mad_i64|mul_lo_u32x)")
+QUARTER = re.compile(r"^v_(ffbh|ffbl|bcnt)")
 
 
 def slots(op):

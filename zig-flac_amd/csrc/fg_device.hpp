@@ -707,8 +707,20 @@ __device__ __forceinline__ void load_candidate(const uint32_t *stg, uint32_t cst
             };
             if (kind == 0 && chan == 0) put([](int32_t L, int32_t) { return L; });
             else if (kind <= 1) put([](int32_t, int32_t R) { return R; });
-            else if (kind == 2) put([](int32_t L, int32_t R) { return (L + R) >> 1; });
-            else put([](int32_t L, int32_t R) { return L - R; });
+            else if (kind == 2) {
+                // mid: L + R from the two sign-extended halves in one SDWA add, then >> 1 (the
+                // compiler's packed-16-bit form took ~13 issue slots per sample pair, this 3 per sample)
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    const int j = 16 * g + jj;
+                    uint32_t sum;
+                    asm("v_add_u32_sdwa %0, sext(%1), sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+                        : "=v"(sum) : "v"(raw[jj]));
+                    int32_t x = (int32_t)sum >> 1;
+                    if (!FULL && l * 64u + j >= n) x = 0;
+                    s[j] = (ST)x;
+                }
+            } else put([](int32_t L, int32_t R) { return L - R; });
             __builtin_amdgcn_sched_barrier(0);
         }
     } else if constexpr (B == 3) {
@@ -853,15 +865,39 @@ __device__ __forceinline__ ST fixed_residual(ST x, ST q1, ST q2, ST q3, ST q4) {
 // every residual (lane 0's first K samples are warm-ups).  Used where the
 // residuals are consumed on the fly, so the five instantiations behind a
 // uniform switch share no live state but the caller's accumulators.
+// The residual is formed by the difference chain e_{q+1}[i] = e_q[i] - e_q[i-1] (K full-rate
+// subtractions per sample, carried differences d_q = e_q[i-1]) rather than the K-th stencil
+// (x + u4 - 4(u1 + u3) + 6 u2 and the like: two-slot shift-adds and multiplies on gfx950); both
+// are the same polynomial, so the low 32 bits -- all fixed.zig:63-74 keeps -- agree.
 template <int K, typename ST, typename F>
 __device__ __forceinline__ void residuals_k(const ST (&s)[64], ST h1, ST h2, ST h3, ST h4, uint32_t l, F &&f) {
-    ST q1 = h1, q2 = h2, q3 = h3, q4 = h4;
+    const uint32_t u1 = (uint32_t)h1, u2 = (uint32_t)h2, u3 = (uint32_t)h3, u4 = (uint32_t)h4;
+    // d_q = e_q at the previous sample (the lane's history: the previous lane's last four)
+    uint32_t d0 = u1, d1 = u1 - u2, d2 = u1 - 2u * u2 + u3, d3 = u1 - 3u * u2 + 3u * u3 - u4;
 #pragma unroll
     for (int j = 0; j < 64; j++) {
-        const ST x = s[j];
-        const ST r = fixed_residual<K, ST>(x, q1, q2, q3, q4);
-        q4 = q3; q3 = q2; q2 = q1; q1 = x;
-        f(j, (j < K) && (l == 0), r);
+        const uint32_t e0 = (uint32_t)s[j];
+        uint32_t e = e0;
+        if constexpr (K >= 1) {
+            const uint32_t e1 = e0 - d0;
+            d0 = e0;
+            e = e1;
+            if constexpr (K >= 2) {
+                const uint32_t e2 = e1 - d1;
+                d1 = e1;
+                e = e2;
+                if constexpr (K >= 3) {
+                    const uint32_t e3 = e2 - d2;
+                    d2 = e2;
+                    e = e3;
+                    if constexpr (K >= 4) {
+                        e = e3 - d3;
+                        d3 = e3;
+                    }
+                }
+            }
+        }
+        f(j, (j < K) && (l == 0), (ST)(int32_t)e);
     }
 }
 #define FG_DISPATCH_K(k, CALL)                        \
@@ -961,7 +997,7 @@ template <int W>
 __device__ __forceinline__ uint32_t lpc_coefs(const int64_t (&R)[W + 1], uint32_t Q, int32_t *tab, uint32_t lane,
                                               uint32_t n, uint32_t bps) {
 #pragma clang fp contract(off)
-    double r[W + 1], a[W], tmp[W], mine[W], myerr = 0.0;
+    double r[W + 1], a[W], mine[W], myerr = 0.0;
 #pragma unroll
     for (int i = 0; i <= W; i++) r[i] = (double)R[i];
 #pragma unroll
@@ -981,13 +1017,16 @@ __device__ __forceinline__ uint32_t lpc_coefs(const int64_t (&R)[W + 1], uint32_
                 acc = acc - p;
             }
             const double k = acc / err;
+            // a[t] -= k a[m-1-t] for t < m, in symmetric pairs (t, m-1-t) so that only two new
+            // values are live at a time (each element's operations and rounding unchanged)
 #pragma unroll
-            for (int t = 0; t < m; t++) {
-                const double p = k * a[m - 1 - t];
-                tmp[t] = a[t] - p;
+            for (int t = 0; t < m / 2; t++) {
+                const double lo = a[t] - k * a[m - 1 - t];
+                const double hi = a[m - 1 - t] - k * a[t];
+                a[t] = lo;
+                a[m - 1 - t] = hi;
             }
-#pragma unroll
-            for (int t = 0; t < m; t++) a[t] = tmp[t];
+            if (m & 1) a[m / 2] = a[m / 2] - k * a[m / 2];
             a[m] = k;
             const bool me = lane == (uint32_t)m;
             have = have || me;
@@ -1112,12 +1151,16 @@ __device__ __forceinline__ void residuals_lpc_inplace(ST (&s)[64], const ST (&hs
 // (exact when the caller's magnitude bound holds).  Per 16-sample group g: S += |e|,
 // T |= e ^ (e >> 31) (= zz >> 1), N |= e (bit 31: some e < 0); lane 0's first `nwarm`
 // samples (warm-ups) are left out.
-template <int W, int LPWX>
-__device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int32_t (&hs)[LPWX], const int32_t (&c)[LPWX],
+template <int W, int LPWX, bool KEEP = false>
+__device__ __forceinline__ void lpc_fast_pass(int32_t (&x)[64], const int32_t (&hs)[LPWX], const int32_t (&c)[LPWX],
                                               uint32_t shift, uint32_t nwarm, uint64_t (&S)[4], uint32_t (&T)[4],
                                               uint32_t (&N)[4]) {
+    // KEEP: descending, each residual's low word written over its sample (a prediction reads only
+    // the samples below it, none of them overwritten yet), so the caller holds the residuals for
+    // the exact-bits pass instead of recomputing them
 #pragma unroll
-    for (int j = 0; j < 64; j++) {
+    for (int jj = 0; jj < 64; jj++) {
+        const int j = KEEP ? 63 - jj : jj;
         int64_t acc = 0;
 #pragma unroll
         for (int t = 0; t < W; t++) {
@@ -1127,6 +1170,7 @@ __device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int3
         }
         const uint32_t plo = __builtin_amdgcn_alignbit((uint32_t)((uint64_t)acc >> 32), (uint32_t)acc, shift);
         uint32_t e = (uint32_t)x[j] - plo;
+        if (KEEP) x[j] = (int32_t)e;
         const uint32_t sg = (uint32_t)((int32_t)e >> 31);
         uint32_t t = e ^ sg;
         uint32_t av = t - sg;
@@ -1139,7 +1183,7 @@ __device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int3
         S[j >> 4] += av;
         T[j >> 4] |= t;
         N[j >> 4] |= e;
-        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound the scheduler's hoisting
+        if ((jj & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound the scheduler's hoisting
     }
 }
 
@@ -1164,6 +1208,9 @@ __device__ __forceinline__ void lpc_fast_pass(const int32_t (&x)[64], const int3
 #define FG_PACK_MINW 4
 #endif
 
+#ifndef FG_BO_FUSED
+#define FG_BO_FUSED 1
+#endif
 #ifndef FG_JOB_LDS
 #define FG_JOB_LDS 1  // the next job records in an LDS ring instead of registers
 #endif
@@ -1367,10 +1414,21 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         }
 
         // ---- 4. CONSTANT / VERBATIM defaults (encoder.zig:493-514)
+        // Full 16-bit frames (FUSED below): no separate all-equal pass -- bestOrder's order-1 sum
+        // T[1] = sum_{i >= 1} |x[i] - x[i-1]| (exact) is zero iff every sample equals x[0], so the
+        // CONSTANT decision is taken from it after step 5 (a constant frame runs bestOrder for
+        // nothing; 128 VALU slots per wave-frame saved on every other frame)
+        constexpr bool EQ_FROM_T1 = FULL && CLS == 16 && FG_BO_FUSED;
         bool try_fixed = false;
+        ST x0c = 0;
         if (bps == 0) {
             R.type = 0;
             R.est = 0;
+        } else if (EQ_FROM_T1) {
+            x0c = (ST)rdl((uint32_t)s[0], 0);
+            R.type = 1;
+            R.est = (uint64_t)n * bps;
+            try_fixed = true;
         } else {
             ST x0;
             if constexpr (CLS != 32) x0 = (ST)rdl((uint32_t)s[0], 0);
@@ -1407,9 +1465,6 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // Full 16-bit frames: bestOrder accumulates |e_q| per 16-sample group (the finest Rice
         // partitions) for every order, so the chosen order's partition sums come out of it and
         // the second residual pass only ORs zigzags (the escape widths).
-#ifndef FG_BO_FUSED
-#define FG_BO_FUSED 1
-#endif
 #ifndef FG_DESC_SUB
 #define FG_DESC_SUB 1  // two-channel builds: SubDesc fixed fields in one six-lane store (r4s: WRITE 0.68 -> 0.50 GB)
 #endif
@@ -1572,6 +1627,12 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             for (int q = 1; q < 5; q++)
                 if (T[q] < T[k]) k = q;  // first minimum (fixed.zig:164)
             if (CLS == 32 && T[k] == ~0ull) try_fixed = false;  // null -> VERBATIM (encoder.zig:520)
+            if (EQ_FROM_T1 && T[1] == 0) {  // all samples equal x[0]: CONSTANT (encoder.zig:497-503)
+                R.type = 0;
+                R.est = bps;
+                R.cval = (int64_t)x0c;
+                try_fixed = false;
+            }
         }
         STAMP(3);
 
@@ -1678,6 +1739,45 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     r0 = rdl64(Sl[3], 0); r1 = rdl64(Sl[3], 16); r2 = rdl64(Sl[3], 32); r3 = rdl64(Sl[3], 48);
                 }
                 const uint32_t m0 = rdl(Wl[3], 0), m1 = rdl(Wl[3], 16), m2 = rdl(Wl[3], 32), m3 = rdl(Wl[3], 48);
+                {
+                    // Orders 5..2 (32 + 16 + 8 + 4 partitions of 2..16 lanes each): one partition per
+                    // lane -- lanes 0-31 order 5, 32-47 order 4, 48-55 order 3, 56-59 order 2 --
+                    // instead of every lane evaluating all four orders (three closed-form Rice
+                    // decisions, ~130 issue slots, fewer per wave-frame).  A group's sum sits in every
+                    // lane of the group; the lane the partition reads it from is chosen so the source
+                    // sets are disjoint (order 5: odd lanes; 4: 2 mod 4; 3: 4 mod 8; 2: 8 mod 16), so
+                    // each source lane exposes one level and one ds_bpermute moves them all.
+                    const uint32_t lvl = l < 32u ? 0u : (l < 48u ? 1u : (l < 56u ? 2u : 3u));
+                    const uint32_t jp = l - (l < 32u ? 0u : (l < 48u ? 32u : (l < 56u ? 48u : 56u)));
+                    const uint32_t tz = (uint32_t)__builtin_ctz(l | 16u);
+                    const SW Se = tz == 0u ? Sl[0] : (tz == 1u ? Sl[1] : (tz == 2u ? Sl[2] : Sl[3]));
+                    const uint32_t We = tz == 0u ? Wl[0] : (tz == 1u ? Wl[1] : (tz == 2u ? Wl[2] : Wl[3]));
+                    const int src4 = (int)(((jp << (lvl + 1u)) + (1u << lvl)) << 2);
+                    SW Sx;
+                    if constexpr (sizeof(SW) == 4) {
+                        Sx = (SW)__builtin_amdgcn_ds_bpermute(src4, (int)Se);
+                    } else {
+                        Sx = (SW)(uint32_t)__builtin_amdgcn_ds_bpermute(src4, (int)(uint32_t)Se) |
+                             ((SW)(uint32_t)__builtin_amdgcn_ds_bpermute(src4, (int)(uint32_t)((uint64_t)Se >> 32)) << 32);
+                    }
+                    const uint32_t Wx = (uint32_t)__builtin_amdgcn_ds_bpermute(src4, (int)We);
+                    const uint32_t oo = 5u - lvl;
+                    const uint32_t len = (128u << lvl) - (jp == 0u ? kw : 0u);
+                    uint32_t cc;
+                    const uint32_t p = rice_choose(Sx, len, Wx, maxp, &cc);
+                    const bool act = l < 60u;
+                    if (act) pb[(1u << oo) - 1u + jp] = (uint8_t)p;
+                    const uint64_t fb = __ballot(act && p < 0x80u && p > 14u);
+                    const uint32_t rA = row_sum32(l < 56u ? cc : 0u), rB = row_sum32((l >= 56u && act) ? cc : 0u);
+                    tots[5] = (uint64_t)rdl(rA, 0) + rdl(rA, 16);
+                    tots[4] = rdl(rA, 32);
+                    tots[3] = rdl(rA, 48);
+                    tots[2] = rdl(rB, 48);
+                    fives[5] = (maxp > 14u && (fb & 0xFFFFFFFFull)) ? 1u : 0u;
+                    fives[4] = (maxp > 14u && ((fb >> 32) & 0xFFFFull)) ? 1u : 0u;
+                    fives[3] = (maxp > 14u && ((fb >> 48) & 0xFFull)) ? 1u : 0u;
+                    fives[2] = (maxp > 14u && ((fb >> 56) & 0xFull)) ? 1u : 0u;
+                }
 #pragma unroll
                 for (int o = 0; o < 9; o++) {
                     if (true) {  // every order unconditionally: straight-line code the scheduler can interleave (o > P is never selected)
@@ -1701,17 +1801,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                             }
                             tots[o] = wave_sum32(cost);
                         } else if (o >= 2) {
-                            const int g = 6 - o;  // a partition spans 2^g lanes
-                            const uint32_t j = l >> g;
-                            const bool lead = (l & ((1u << g) - 1u)) == 0;
-                            const uint32_t len = (4096u >> o) - (j == 0 ? kw : 0u);
-                            const uint32_t p = rice_choose(Sl[g - 1], len, Wl[g - 1], maxp, &c);
-                            if (lead) {
-                                cost = c;
-                                five = (p < 0x80u && p > 14u);
-                                pb[(1u << o) - 1u + j] = (uint8_t)p;
-                            }
-                            tots[o] = wave_sum32(cost);
+                            // orders 5..2: computed once for all four below the loop head
                         } else {
                             // uniform: order 1 = rows {0,1} and {2,3}; order 0 = all rows
                             const uint32_t len0 = (4096u >> o) - kw, len1 = 4096u >> o;
@@ -1727,7 +1817,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                             five = (p0 < 0x80u && p0 > 14u) || (o == 1 && p1 < 0x80u && p1 > 14u);
                             tots[o] = (uint64_t)c0 + c1;
                         }
-                        fives[o] = (maxp > 14u && __any(five)) ? 1u : 0u;
+                        if (o < 2 || o > 5) fives[o] = (maxp > 14u && __any(five)) ? 1u : 0u;
                     }
                 }
             } else {
@@ -1798,8 +1888,18 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 for (int g = 0; g < 4; g++)
                     S8[g] = k == 0 ? tg[0][g] : k == 1 ? tg[1][g] : k == 2 ? tg[2][g] : k == 3 ? tg[3][g] : tg[4][g];
                 if (!FP && k >= 3) S8[0] = ((const uint32_t *)par)[(k == 3 ? 0u : 64u) + l];  // stashed above
-                auto acc = [&](int j, bool warm, SS r) { O8[j >> 4] |= warm ? 0u : zigzag32((int32_t)r); };
+                // escape widths: bitlen(OR of zigzags) == bitlen(largest zigzag) = bitlen(max(2 max e,
+                // -2 min e - 1)) -- a running max/min per group (v_max3 / v_min3 over sample pairs:
+                // 2 issue slots a sample) instead of a zigzag and an OR per sample (4-5)
+                int32_t mx[4] = {0, 0, 0, 0}, mn[4] = {0, 0, 0, 0};
+                auto acc = [&](int j, bool warm, SS r) {
+                    const int32_t v = warm ? 0 : (int32_t)r;
+                    mx[j >> 4] = max(mx[j >> 4], v);
+                    mn[j >> 4] = min(mn[j >> 4], v);
+                };
                 FG_DISPATCH_K(k, (residuals_k<K, SS>(s, hl1, hl2, hl3, hl4, l, acc)))
+#pragma unroll
+                for (int g = 0; g < 4; g++) O8[g] = (uint32_t)max(2 * mx[g], -2 * mn[g] - 1);
             } else {
                 auto acc = [&](int j, bool warm, SS r) { part_acc(S8, O8, ps, j, warm, (int32_t)r); };
                 FG_DISPATCH_K(k, (residuals_k<K, SS>(s, hl1, hl2, hl3, hl4, l, acc)))
@@ -1821,6 +1921,14 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             }
         }
         int32_t *ltab = nullptr;
+        // LKEEP (full 32-bit frames, c5): the fast LPC pass leaves the residuals in its sample
+        // registers and, when LPC wins, the exact data bits of the lane's segment are taken from
+        // them right after the parameter search (lseg), so step 10 neither reloads the samples nor
+        // recomputes 64 q-tap predictions per lane -- for the two written candidates that pass
+        // sat on the frame's critical path (15 % of a c5 analysis wave's time, r4n stamps)
+        constexpr bool LKEEP = FULL && LPW > 0 && CLS == 32;
+        uint32_t lseg = 0;
+        bool lkept = false;
         if constexpr (LPW > 0) {
             // ---- 8b. LPC order search (oracle/flac_oracle.c lpc_search): every order 1..Q with
             // usable coefficients; total = rice + q (bps' + 15) + 9; strictly smaller replaces
@@ -1830,6 +1938,10 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 STAMP(11);  // (stamps build: the fixed predictor's search ends here)
                 bool fits;
                 uint32_t qsel = 0;  // the order selected by its LD error (contract step 7)
+                // the samples are reloaded from the staging here: a memory clobber keeps the compiler
+                // from proving this load equal to step 2's (same LDS words, same waste shift) and
+                // holding those 64 registers live through steps 5-8, where they spilled
+                asm volatile("" ::: "memory");
                 {
                     int32_t x[64];
                     fits = __all(load_lpc_samples<B, CLS, FULL, NC>(stg, cst, l, n, stereo, cand, C, R.waste, x));
@@ -1878,9 +1990,9 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                                 uint64_t S8[4] = {0, 0, 0, 0};
                                 uint32_t T8[4] = {0, 0, 0, 0}, N8[4] = {0, 0, 0, 0};
                                 const uint32_t nw = l == 0 ? q : 0u;
-                                if (q <= 4u) lpc_fast_pass<4, LPW>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
-                                else if (LPW <= 8 || q <= 8u) lpc_fast_pass<(LPW < 8 ? LPW : 8), LPW>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
-                                else lpc_fast_pass<LPW, LPW>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
+                                if (q <= 4u) lpc_fast_pass<4, LPW, LKEEP>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
+                                else if (LPW <= 8 || q <= 8u) lpc_fast_pass<(LPW < 8 ? LPW : 8), LPW, LKEEP>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
+                                else lpc_fast_pass<LPW, LPW, LKEEP>(x, hs, c, (uint32_t)shq, nw, S8, T8, N8);
                                 const uint32_t tall = (uint32_t)__builtin_amdgcn_readfirstlane(
                                     (int)wave_or32(T8[0] | T8[1] | T8[2] | T8[3]));
                                 STAMP(14);
@@ -1908,6 +2020,47 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                                     R.method = best_m;
                                     R.lsh = shq;
                                     cur ^= 1u;
+                                    if constexpr (LKEEP) {
+                                        // step 10's data bits (frame_writer.zig:299-372) from the residuals
+                                        // in x: per 16-sample group the quotients, cnt (1 + p) or an escape's
+                                        // cnt * width, and the partition headers the lane opens
+                                        const uint32_t sh = 12u - best_o, psz = 4096u >> best_o;
+                                        const uint32_t plen = 4u + best_m;
+                                        const uint8_t *pp = par + cur * 512u + ((1u << best_o) - PO);
+                                        uint32_t pq[4], qa[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                                        for (int g = 0; g < 4; g++) pq[g] = pp[(l * 64u + 16u * g) >> sh];
+                                        if (__all(pq[0] != 0u && pq[1] != 0u && pq[2] != 0u && pq[3] != 0u)) {
+                                            uint32_t sm[4];
+#pragma unroll
+                                            for (int g = 0; g < 4; g++) sm[g] = (pq[g] - 1u) & 31u;
+#pragma unroll
+                                            for (int j = 0; j < 64; j++) {
+                                                const int32_t e = x[j];
+                                                const uint32_t t = (uint32_t)(e ^ (e >> 31));
+                                                const bool warm = j < LPW && l == 0 && (uint32_t)j < q;
+                                                qa[j >> 4] = add_chain(qa[j >> 4], warm ? 0u : (t >> sm[j >> 4]));
+                                            }
+                                        } else {
+#pragma unroll
+                                            for (int j = 0; j < 64; j++) {
+                                                const uint32_t zz = zigzag32(x[j]);
+                                                const bool warm = j < LPW && l == 0 && (uint32_t)j < q;
+                                                qa[j >> 4] = add_chain(qa[j >> 4], warm ? 0u : (zz >> (pq[j >> 4] & 31u)));
+                                            }
+                                        }
+                                        uint32_t sg = 0;
+#pragma unroll
+                                        for (int g = 0; g < 4; g++) {
+                                            const uint32_t pg = pq[g], i = l * 64u + 16u * g;
+                                            const bool esc = (pg & 0x80u) != 0;
+                                            const uint32_t cnt = 16u - ((g == 0 && l == 0) ? q : 0u);
+                                            sg += esc ? cnt * (pg & 0x7Fu) : qa[g] + cnt * (1u + pg);
+                                            if (i != 0 && (i & (psz - 1u)) == 0) sg += plen + (esc ? 5u : 0u);
+                                        }
+                                        lseg = sg;
+                                        lkept = true;
+                                    }
                                 }
                                 continue;
                             }
@@ -2057,7 +2210,9 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                         FG_DISPATCH_K(k, (residuals_k<K, SS>(t, g1, g2, g3, g4, l, f)))
                     }
                 };
-                if constexpr (FULL) {
+                if (LKEEP && lkept && R.type == 3) {
+                    seg = lseg;  // from the order search's registers (LKEEP above)
+                } else if constexpr (FULL) {
                     const uint32_t sh = 12u - o, psz = 4096u >> o;
                     uint32_t pq[4];
 #pragma unroll
@@ -2066,11 +2221,26 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     // the unary stop bits and low bits (cnt * (1 + p)), an escape group's
                     // cnt * width and the partition headers are added once per group
                     uint32_t qa[4] = {0u, 0u, 0u, 0u};
-                    auto len_a = [&](int j, bool warm, ST r) {
-                        const uint32_t zz = zigzag32((int32_t)r);
-                        qa[j >> 4] = add_chain(qa[j >> 4], warm ? 0u : (zz >> (pq[j >> 4] & 31u)));
-                    };
-                    pass(len_a);
+                    if (__all(pq[0] != 0u && pq[1] != 0u && pq[2] != 0u && pq[3] != 0u)) {
+                        // no Rice parameter 0 in the wave (escape groups' quotients are unused): the
+                        // quotient zz >> p = (2t + sign) >> p = t >> (p - 1) with t = e ^ (e >> 31),
+                        // two issue slots less per sample than forming the zigzag
+                        uint32_t sm[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) sm[q] = (pq[q] - 1u) & 31u;
+                        auto len_t = [&](int j, bool warm, ST r) {
+                            const int32_t e = (int32_t)r;
+                            const uint32_t t = (uint32_t)(e ^ (e >> 31));
+                            qa[j >> 4] = add_chain(qa[j >> 4], warm ? 0u : (t >> sm[j >> 4]));
+                        };
+                        pass(len_t);
+                    } else {
+                        auto len_a = [&](int j, bool warm, ST r) {
+                            const uint32_t zz = zigzag32((int32_t)r);
+                            qa[j >> 4] = add_chain(qa[j >> 4], warm ? 0u : (zz >> (pq[j >> 4] & 31u)));
+                        };
+                        pass(len_a);
+                    }
 #pragma unroll
                     for (int g = 0; g < 4; g++) {
                         const uint32_t p = pq[g], i = l * 64u + 16u * g;
