@@ -1926,7 +1926,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
         // them right after the parameter search (lseg), so step 10 neither reloads the samples nor
         // recomputes 64 q-tap predictions per lane -- for the two written candidates that pass
         // sat on the frame's critical path (15 % of a c5 analysis wave's time, r4n stamps)
-        constexpr bool LKEEP = FULL && LPW > 0 && CLS == 32;
+        constexpr bool LKEEP = FULL && LPW > 0 && (CLS == 32 || CLS == 24);
         uint32_t lseg = 0;
         bool lkept = false;
         if constexpr (LPW > 0) {
