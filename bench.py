@@ -311,6 +311,21 @@ def kernel_times(enc):
     return {name: enc.kernel_time(k) for k, name in enumerate(flacgpu.KERNEL_NAMES)}
 
 
+def read_valu_mix(cfg, kernel):
+    """SIMD-cycles per VALU instruction of `kernel` in config `cfg` from the committed static-mix
+    summary (tools/valu_mix.sh -> profiles/<tag>_valu_mix.json, priced with the measured issue rates
+    of profiles/r5_issue_micro.txt), else None."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*valu_mix*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        v = (d.get(cfg) or {}).get(kernel)
+        if v:
+            return v.get("cycles_per_instr"), os.path.basename(f)
+    return None, None
+
+
 def read_pmc(key, kernel):
     """(HBM bytes per launch, counters) of `kernel` in the committed PMC summary of workload `key`."""
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
@@ -750,6 +765,7 @@ def cpu_baseline(buf, args):
 # ---------------------------------------------------------------------------------------------
 # roofline of one configuration's step, from HIP events (bench) + the committed PMC summary
 VALU_PEAK = 1024 * 0.5 * 2.4e9  # wave64 VALU instructions/s: 1024 SIMD-32s x 1 per 2 cycles x 2.4 GHz
+SIMD_CYCLES_PER_S = 1024 * 2.4e9  # SIMD-cycles per second over the chip (weighted issue: tools/valu_rates.py)
 
 
 def roofline_of(args, kt, steps, pcm_bytes, out_bytes, ms_per_step, key):
@@ -775,18 +791,28 @@ def roofline_of(args, kt, steps, pcm_bytes, out_bytes, ms_per_step, key):
         traffic, counters, src = read_pmc(key, k)
         issue = None
         if counters.get("SQ_INSTS_VALU"):
+            cpi, msrc = read_valu_mix(args.config or "c2", k)
             issue = {"valu_wave_instr_per_launch": counters["SQ_INSTS_VALU"], "peak_valu_wave_instr_per_s": VALU_PEAK,
                      "valu_issue_frac": round(counters["SQ_INSTS_VALU"] / avg / VALU_PEAK, 4),
+                     # SIMD-cycles the mix needs at the measured per-opcode rates / SIMD-cycles available
+                     "weighted_issue_frac": round(counters["SQ_INSTS_VALU"] * cpi / avg / SIMD_CYCLES_PER_S, 4)
+                     if cpi else None, "cycles_per_instr": cpi, "mix_source": msrc,
                      "waves_per_launch": counters.get("SQ_WAVES"), "source": src}
         return {"achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(avg * 1e3, 4),
                 "algorithmic_bytes_per_launch": algo[k], "traffic": traffic, "traffic_source": src,
                 "traffic_ratio": round(traffic / algo[k], 3) if traffic else None, "issue": issue}
 
+    wcyc_step, wcyc_ok = 0.0, True
     for k in per_launch:
         _, counters, src = read_pmc(key, k)
         if counters.get("SQ_INSTS_VALU"):
             valu_step += counters["SQ_INSTS_VALU"] * lps[k]
             valu_src = src
+            cpi, _ = read_valu_mix(args.config or "c2", k)
+            if cpi:
+                wcyc_step += counters["SQ_INSTS_VALU"] * lps[k] * cpi
+            elif k in ("analyze", "pack", "md5"):
+                wcyc_ok = False
         elif k in ("analyze", "pack", "md5"):
             valu_missing.append(k)
     enc_k = [k for k in ("analyze", "pack") if k in per_launch]
@@ -795,9 +821,15 @@ def roofline_of(args, kt, steps, pcm_bytes, out_bytes, ms_per_step, key):
     rk = {k: kernel_roofline(k) for k in ("analyze", "pack", "md5") if k in per_launch}
     achieved = algo[dom] / per_launch[dom] / 1e9
     step_issue = round(valu_step / (VALU_PEAK * ms_per_step / 1e3), 4) if valu_step and not valu_missing else None
+    weighted = (round(wcyc_step / (SIMD_CYCLES_PER_S * ms_per_step / 1e3), 4)
+                if valu_step and not valu_missing and wcyc_ok and wcyc_step else None)
     return {
         "bound": "valu-issue",
         "step_issue_frac": step_issue,
+        "weighted_issue_frac": weighted,
+        "weighted_issue_note": "Sigma SQ_INSTS_VALU x SIMD-cycles per instruction of each kernel's mix (measured "
+                               "per-opcode rates, profiles/r5_issue_micro.txt; static mix, tools/valu_rates.py) / "
+                               "(1024 SIMDs x 2.4 GHz x ms_per_step)",
         "step_issue_note": ("Sigma SQ_INSTS_VALU per launch x launches per step over every kernel of the step "
                             f"({valu_src}) / ({VALU_PEAK:.4g} wave-instr/s x ms_per_step)" if step_issue is not None
                             else f"no committed PMC summary for workload {key} (kernels {valu_missing})"),
@@ -901,7 +933,8 @@ def _compact_roofline(r):
     ks = {}
     for k, v in (r.get("kernels") or {}).items():
         ks[k] = {"ms": v.get("avg_launch_ms"), "frac": _r(v.get("frac")), "traffic_ratio": v.get("traffic_ratio"),
-                 "issue": (v.get("issue") or {}).get("valu_issue_frac")}
+                 "issue": (v.get("issue") or {}).get("valu_issue_frac"),
+                 "w_issue": (v.get("issue") or {}).get("weighted_issue_frac")}
     out = {"bound": r.get("bound"), "kernel": r.get("kernel"), "achieved": r.get("achieved"), "peak": r.get("peak"),
            "unit": r.get("unit"), "frac": r.get("frac"), "traffic": r.get("traffic"),
            "traffic_ratio": (r.get("kernels") or {}).get(_dom_name(r), {}).get("traffic_ratio"),
@@ -953,6 +986,7 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
         cs[c["config"]] = {"value": c.get("value"), "ms_per_step": c.get("ms_per_step"),
                            "kernel_ms": c.get("kernel_ms_per_step"), "frac": r.get("frac"),
                            "step_issue_frac": r.get("step_issue_frac"),
+                           "weighted_issue_frac": r.get("weighted_issue_frac"),
                            "traffic_ratio": (r.get("kernels") or {}).get(_dom_name(r), {}).get("traffic_ratio"),
                            "output_ok": c.get("output_ok"), "cpu": cb.get("value"),
                            "cpu_single_core": (cb.get("single_core") or {}).get("value")}

@@ -89,8 +89,9 @@ __host__ __device__ inline PackLayout pack_layout(uint32_t C, uint32_t B, uint32
     r0 = fg_round16(r0);
     L.buf0 = 0;
     L.buf1 = dbuf ? r0 : 0u;
+    // (until round 5 a 4-KiB CRC table area sat here; the table-free CRC of round 3 left it unused)
     L.crc = dbuf ? 2u * r0 : r0;
-    L.misc = L.crc + 4096u;
+    L.misc = L.crc;
     L.total = fg_round16(L.misc + 256u);
     return L;
 }
@@ -133,8 +134,9 @@ __host__ __device__ inline PackLayout packw_layout(uint32_t C, uint32_t B, uint3
     r0 = fg_round16(r0);
     L.buf0 = 0;
     L.buf1 = dbuf ? r0 : 0u;
+    // (until round 5 a 4-KiB CRC table area sat here; the table-free CRC of round 3 left it unused)
     L.crc = dbuf ? 2u * r0 : r0;
-    L.misc = L.crc + 4096u;
+    L.misc = L.crc;
     L.total = fg_round16(L.misc + 256u);
     return L;
 }
