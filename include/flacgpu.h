@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define FLACGPU_ABI_VERSION 3
+#define FLACGPU_ABI_VERSION 4
 
 /* the HIP null (legacy default) stream as a hip_stream argument */
 #define FLACGPU_STREAM_LEGACY ((void *)1)
@@ -249,14 +249,16 @@ int flacgpu_md5_plan_host(const flacgpu_plan *plan, const void *h_pcm, flacgpu_m
 int flacgpu_plan_md5_engine(const flacgpu_plan *plan);
 
 /* The rates the engine choice is priced with (no reference
- * counterpart: the reference hashes on its one thread).  host_chain[k - 1]: bytes/s
- * per pool worker when every worker interleaves k chains (k = 1..4), MEASURED on
- * this machine by running the pool the first time they are needed
+ * counterpart: the reference hashes on its one thread).  host_chain[i]: bytes/s
+ * per pool worker when every worker holds host_chains[i] chains (1, 2, 3, 4 for the
+ * scalar interleave; 1, 4, 8, 16 where the host has AVX-512), MEASURED on this
+ * machine by running the pool the first time they are needed
  * (flacgpu_md5_get_rates); host_workers: the pool's size (0: no pool, host_chain
  * is one chain on the caller); device_lane / device_chip: bytes/s of one stream's
  * GPU lane beside the encode and of all lanes together (MI355X measurements). */
 typedef struct {
     double host_chain[4];
+    uint32_t host_chains[4]; /* chains per worker of each host_chain entry (0s: 1, 2, 3, 4) */
     double device_lane;
     double device_chip;
     int32_t host_workers;
@@ -268,7 +270,8 @@ int flacgpu_md5_get_rates(flacgpu_md5_rates *out);
 int flacgpu_md5_set_rates(const flacgpu_md5_rates *rates);
 /* The engine the rates predict faster for n_streams chains of at most max_len
  * bytes, total_len bytes in all: host time = total / (pool throughput at
- * ceil(n / workers) chains per worker, time-sliced past 4), device time =
+ * ceil(n / workers) chains per worker, interpolated between the measured points
+ * and flat past the last: time-sliced), device time =
  * max(max_len / device_lane, total / device_chip).  Needs no GPU. */
 int flacgpu_md5_engine_for(uint32_t n_streams, uint64_t max_len, uint64_t total_len);
 

@@ -148,3 +148,24 @@ def test_md5_rates_measured_on_first_use():
     assert all(v > 1e7 for v in r.host_chain)  # any host hashes > 10 MB/s
     assert r.host_chain[3] > r.host_chain[0]  # interleaving four chains beats one on a core
     assert r.host_workers >= 0
+
+
+@pytest.mark.parametrize("avx512", ["0", "1"])
+def test_md5_many_vector_and_scalar_paths(avx512):
+    """The pool's AVX-512 sixteen-chain path (compress_x16) and the scalar interleave give
+    hashlib's digests for 1..70 chains of mixed lengths (partial blocks, empty chains) on 3 workers
+    -- lane counts 1..16 and time slicing past 48 chains.  In a child: the path is chosen once."""
+    _lib_or_skip()
+    import subprocess
+
+    code = ("import sys, hashlib, random; sys.path.insert(0, %r); import flacgpu; r = random.Random(5);"
+            "ok = True\n"
+            "for n in (1, 2, 5, 16, 17, 33, 70):\n"
+            "    c = [bytes(r.getrandbits(8) for _ in range(r.choice([0, 63, 4096, 4160, 70000, 131072 + 7])))"
+            " for _ in range(n)]\n"
+            "    ok &= flacgpu.md5_many(c) == [hashlib.md5(x).digest() for x in c]\n"
+            "print('ok' if ok else 'BAD')"
+            % os.path.join(os.path.dirname(__file__), "..", "zig-flac_amd"))
+    env = dict(os.environ, FLACGPU_MD5_THREADS="3", FLACGPU_MD5_AVX512=avx512)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr

@@ -1325,7 +1325,7 @@ static flacgpu_md5_rates md5_rates() {
     std::lock_guard<std::mutex> lk(g_rates_mu);
     if (!g_rates_set) {
         flacgpu_md5_rates r{};
-        fg::md5_measure_rates(r.host_chain);
+        fg::md5_measure_rates(r.host_chain, r.host_chains);
         r.device_lane = 72e6;
         r.device_chip = 600e9;
         r.host_workers = fg::md5_pool_workers();
@@ -1352,6 +1352,13 @@ int flacgpu_md5_set_rates(const flacgpu_md5_rates *r) {
     if (r) {
         g_rates = *r;
         g_rates.measured = 2;
+        if (!g_rates.host_chains[0])
+            for (uint32_t i = 0; i < 4; i++) g_rates.host_chains[i] = i + 1u;
+        for (uint32_t i = 1; i < 4; i++)
+            if (g_rates.host_chains[i] <= g_rates.host_chains[i - 1]) {
+                g_rates_set = false;
+                return FLACGPU_ERR_INVALID_INPUT;
+            }
     }
     g_rates_set = r != nullptr;
     return FLACGPU_OK;
@@ -1366,11 +1373,25 @@ int flacgpu_md5_engine_for(uint32_t n_streams, uint64_t max_len, uint64_t total_
     if (r.host_workers <= 0) {
         t_host = (double)total_len / r.host_chain[0];  // no pool: the caller hashes chain after chain
     } else {
-        // k chains per worker (time-sliced past four: the pool's throughput stays at k = 4); with
-        // fewer chains than workers, one chain each on n workers
+        // k chains per worker: the per-worker rate interpolated between the measured points, flat
+        // past the last (more chains are time-sliced); with fewer chains than workers, one chain
+        // each on n workers
         const double w = r.host_workers;
-        const int k = (int)std::min(4.0, std::ceil(n / w));
-        t_host = std::max((double)total_len / (r.host_chain[k - 1] * std::min(n, w)), (double)max_len / r.host_chain[0]);
+        const double k = std::ceil(n / w);
+        double rw = r.host_chain[3];
+        for (int i = 0; i < 4; i++) {
+            const double pk = r.host_chains[i] ? r.host_chains[i] : i + 1.0;
+            if (k <= pk) {
+                if (i == 0) {
+                    rw = r.host_chain[0];
+                } else {
+                    const double p0 = r.host_chains[i - 1] ? r.host_chains[i - 1] : i;
+                    rw = r.host_chain[i - 1] + (r.host_chain[i] - r.host_chain[i - 1]) * (k - p0) / (pk - p0);
+                }
+                break;
+            }
+        }
+        t_host = std::max((double)total_len / (rw * std::min(n, w)), (double)max_len / r.host_chain[0]);
     }
     return t_host < t_dev ? FLACGPU_MD5_HOST : FLACGPU_MD5_DEVICE;
 }

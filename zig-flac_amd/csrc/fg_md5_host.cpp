@@ -7,6 +7,8 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -137,6 +139,124 @@ void compress_n(uint32_t *const st[N], const uint8_t *const blk0[N], size_t nblo
     }
 }
 
+// Up to 16 independent chains in the 16 dword lanes of AVX-512 registers (lane j = chain j): one
+// step of all of them is five vector instructions (vpternlogd computes F/G/H/I in one), so a core
+// advances 16 chains at the latency of one -- the scalar interleave above runs out of issue width
+// at about four.  Message words reach their lanes by a 16 x 16 dword transpose of the chains' next
+// blocks.  Chains j >= n read a zero block and are not stored.  Compiled for AVX-512F only (the
+// rest of the library stays baseline x86-64); avx512_on() picks it at run time.
+#define M5X_F(b, c, d) _mm512_ternarylogic_epi32(b, c, d, 0xCA)  // b ? c : d
+#define M5X_G(b, c, d) _mm512_ternarylogic_epi32(d, b, c, 0xCA)  // d ? b : c
+#define M5X_H(b, c, d) _mm512_ternarylogic_epi32(b, c, d, 0x96)  // b ^ c ^ d
+#define M5X_I(b, c, d) _mm512_ternarylogic_epi32(b, c, d, 0x39)  // c ^ (b | ~d)
+#define M5X_STEP(F, a, b, c, d, x, k, s)                                                                     \
+    a = _mm512_add_epi32(b, _mm512_rol_epi32(_mm512_add_epi32(_mm512_add_epi32(a, F(b, c, d)),               \
+                                                              _mm512_add_epi32(x, _mm512_set1_epi32((int)(k)))), s))
+
+__attribute__((target("avx512f"))) static inline void m5x_transpose(__m512i (&m)[16]) {
+    __m512i t[16];
+    for (int i = 0; i < 16; i += 2) {
+        t[i] = _mm512_unpacklo_epi32(m[i], m[i + 1]);
+        t[i + 1] = _mm512_unpackhi_epi32(m[i], m[i + 1]);
+    }
+    for (int i = 0; i < 16; i += 4) {
+        m[i] = _mm512_unpacklo_epi64(t[i], t[i + 2]);
+        m[i + 1] = _mm512_unpackhi_epi64(t[i], t[i + 2]);
+        m[i + 2] = _mm512_unpacklo_epi64(t[i + 1], t[i + 3]);
+        m[i + 3] = _mm512_unpackhi_epi64(t[i + 1], t[i + 3]);
+    }
+    for (int i = 0; i < 4; i++) {
+        t[i] = _mm512_shuffle_i32x4(m[i], m[i + 4], 0x88);
+        t[i + 4] = _mm512_shuffle_i32x4(m[i], m[i + 4], 0xDD);
+        t[i + 8] = _mm512_shuffle_i32x4(m[i + 8], m[i + 12], 0x88);
+        t[i + 12] = _mm512_shuffle_i32x4(m[i + 8], m[i + 12], 0xDD);
+    }
+    for (int i = 0; i < 4; i++) {
+        m[i] = _mm512_shuffle_i32x4(t[i], t[i + 8], 0x88);
+        m[i + 8] = _mm512_shuffle_i32x4(t[i], t[i + 8], 0xDD);
+        m[i + 4] = _mm512_shuffle_i32x4(t[i + 4], t[i + 12], 0x88);
+        m[i + 12] = _mm512_shuffle_i32x4(t[i + 4], t[i + 12], 0xDD);
+    }
+}
+
+__attribute__((target("avx512f"))) void compress_x16(uint32_t *const st[], const uint8_t *const blk0[], int n,
+                                                      size_t nblocks) {
+    alignas(64) static const uint8_t zero[64] = {};
+    alignas(64) uint32_t sa[16], sb[16], sc[16], sd[16];
+    const uint8_t *blk[16];
+    for (int j = 0; j < 16; j++) {
+        const bool on = j < n;
+        sa[j] = on ? st[j][0] : 0u; sb[j] = on ? st[j][1] : 0u; sc[j] = on ? st[j][2] : 0u; sd[j] = on ? st[j][3] : 0u;
+        blk[j] = on ? blk0[j] : zero;
+    }
+    __m512i a0 = _mm512_load_si512(sa), b0 = _mm512_load_si512(sb), c0 = _mm512_load_si512(sc), d0 = _mm512_load_si512(sd);
+    for (size_t nb = 0; nb < nblocks; nb++) {
+        __m512i X[16];
+        for (int j = 0; j < 16; j++) {
+            X[j] = _mm512_loadu_si512((const void *)blk[j]);
+            if (j < n) blk[j] += 64;
+        }
+        // rows (chains) -> columns (message words): afterwards X[w] lane j = word w of chain j
+        m5x_transpose(X);
+        const __m512i *W = X;
+        __m512i a = a0, b = b0, c = c0, d = d0;
+        M5X_STEP(M5X_F, a, b, c, d, W[0], 0xd76aa478, 7);   M5X_STEP(M5X_F, d, a, b, c, W[1], 0xe8c7b756, 12);
+        M5X_STEP(M5X_F, c, d, a, b, W[2], 0x242070db, 17);  M5X_STEP(M5X_F, b, c, d, a, W[3], 0xc1bdceee, 22);
+        M5X_STEP(M5X_F, a, b, c, d, W[4], 0xf57c0faf, 7);   M5X_STEP(M5X_F, d, a, b, c, W[5], 0x4787c62a, 12);
+        M5X_STEP(M5X_F, c, d, a, b, W[6], 0xa8304613, 17);  M5X_STEP(M5X_F, b, c, d, a, W[7], 0xfd469501, 22);
+        M5X_STEP(M5X_F, a, b, c, d, W[8], 0x698098d8, 7);   M5X_STEP(M5X_F, d, a, b, c, W[9], 0x8b44f7af, 12);
+        M5X_STEP(M5X_F, c, d, a, b, W[10], 0xffff5bb1, 17); M5X_STEP(M5X_F, b, c, d, a, W[11], 0x895cd7be, 22);
+        M5X_STEP(M5X_F, a, b, c, d, W[12], 0x6b901122, 7);  M5X_STEP(M5X_F, d, a, b, c, W[13], 0xfd987193, 12);
+        M5X_STEP(M5X_F, c, d, a, b, W[14], 0xa679438e, 17); M5X_STEP(M5X_F, b, c, d, a, W[15], 0x49b40821, 22);
+        M5X_STEP(M5X_G, a, b, c, d, W[1], 0xf61e2562, 5);   M5X_STEP(M5X_G, d, a, b, c, W[6], 0xc040b340, 9);
+        M5X_STEP(M5X_G, c, d, a, b, W[11], 0x265e5a51, 14); M5X_STEP(M5X_G, b, c, d, a, W[0], 0xe9b6c7aa, 20);
+        M5X_STEP(M5X_G, a, b, c, d, W[5], 0xd62f105d, 5);   M5X_STEP(M5X_G, d, a, b, c, W[10], 0x02441453, 9);
+        M5X_STEP(M5X_G, c, d, a, b, W[15], 0xd8a1e681, 14); M5X_STEP(M5X_G, b, c, d, a, W[4], 0xe7d3fbc8, 20);
+        M5X_STEP(M5X_G, a, b, c, d, W[9], 0x21e1cde6, 5);   M5X_STEP(M5X_G, d, a, b, c, W[14], 0xc33707d6, 9);
+        M5X_STEP(M5X_G, c, d, a, b, W[3], 0xf4d50d87, 14);  M5X_STEP(M5X_G, b, c, d, a, W[8], 0x455a14ed, 20);
+        M5X_STEP(M5X_G, a, b, c, d, W[13], 0xa9e3e905, 5);  M5X_STEP(M5X_G, d, a, b, c, W[2], 0xfcefa3f8, 9);
+        M5X_STEP(M5X_G, c, d, a, b, W[7], 0x676f02d9, 14);  M5X_STEP(M5X_G, b, c, d, a, W[12], 0x8d2a4c8a, 20);
+        M5X_STEP(M5X_H, a, b, c, d, W[5], 0xfffa3942, 4);   M5X_STEP(M5X_H, d, a, b, c, W[8], 0x8771f681, 11);
+        M5X_STEP(M5X_H, c, d, a, b, W[11], 0x6d9d6122, 16); M5X_STEP(M5X_H, b, c, d, a, W[14], 0xfde5380c, 23);
+        M5X_STEP(M5X_H, a, b, c, d, W[1], 0xa4beea44, 4);   M5X_STEP(M5X_H, d, a, b, c, W[4], 0x4bdecfa9, 11);
+        M5X_STEP(M5X_H, c, d, a, b, W[7], 0xf6bb4b60, 16);  M5X_STEP(M5X_H, b, c, d, a, W[10], 0xbebfbc70, 23);
+        M5X_STEP(M5X_H, a, b, c, d, W[13], 0x289b7ec6, 4);  M5X_STEP(M5X_H, d, a, b, c, W[0], 0xeaa127fa, 11);
+        M5X_STEP(M5X_H, c, d, a, b, W[3], 0xd4ef3085, 16);  M5X_STEP(M5X_H, b, c, d, a, W[6], 0x04881d05, 23);
+        M5X_STEP(M5X_H, a, b, c, d, W[9], 0xd9d4d039, 4);   M5X_STEP(M5X_H, d, a, b, c, W[12], 0xe6db99e5, 11);
+        M5X_STEP(M5X_H, c, d, a, b, W[15], 0x1fa27cf8, 16); M5X_STEP(M5X_H, b, c, d, a, W[2], 0xc4ac5665, 23);
+        M5X_STEP(M5X_I, a, b, c, d, W[0], 0xf4292244, 6);   M5X_STEP(M5X_I, d, a, b, c, W[7], 0x432aff97, 10);
+        M5X_STEP(M5X_I, c, d, a, b, W[14], 0xab9423a7, 15); M5X_STEP(M5X_I, b, c, d, a, W[5], 0xfc93a039, 21);
+        M5X_STEP(M5X_I, a, b, c, d, W[12], 0x655b59c3, 6);  M5X_STEP(M5X_I, d, a, b, c, W[3], 0x8f0ccc92, 10);
+        M5X_STEP(M5X_I, c, d, a, b, W[10], 0xffeff47d, 15); M5X_STEP(M5X_I, b, c, d, a, W[1], 0x85845dd1, 21);
+        M5X_STEP(M5X_I, a, b, c, d, W[8], 0x6fa87e4f, 6);   M5X_STEP(M5X_I, d, a, b, c, W[15], 0xfe2ce6e0, 10);
+        M5X_STEP(M5X_I, c, d, a, b, W[6], 0xa3014314, 15);  M5X_STEP(M5X_I, b, c, d, a, W[13], 0x4e0811a1, 21);
+        M5X_STEP(M5X_I, a, b, c, d, W[4], 0xf7537e82, 6);   M5X_STEP(M5X_I, d, a, b, c, W[11], 0xbd3af235, 10);
+        M5X_STEP(M5X_I, c, d, a, b, W[2], 0x2ad7d2bb, 15);  M5X_STEP(M5X_I, b, c, d, a, W[9], 0xeb86d391, 21);
+        a0 = _mm512_add_epi32(a0, a);
+        b0 = _mm512_add_epi32(b0, b);
+        c0 = _mm512_add_epi32(c0, c);
+        d0 = _mm512_add_epi32(d0, d);
+    }
+    _mm512_store_si512(sa, a0);
+    _mm512_store_si512(sb, b0);
+    _mm512_store_si512(sc, c0);
+    _mm512_store_si512(sd, d0);
+    for (int j = 0; j < n; j++) {
+        st[j][0] = sa[j]; st[j][1] = sb[j]; st[j][2] = sc[j]; st[j][3] = sd[j];
+    }
+}
+
+// the host supports AVX-512F (checked once); FLACGPU_MD5_AVX512=0 turns the vector path off
+bool avx512_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("FLACGPU_MD5_AVX512");
+        if (e && e[0] == '0') return false;
+        __builtin_cpu_init();
+        return __builtin_cpu_supports("avx512f") != 0;
+    }();
+    return on;
+}
+
 // The process-wide hashing pool (Md5Pool below): a job is one whole-buffer update of a HostMd5.
 struct Md5Job {
     HostMd5 *h;
@@ -248,7 +368,9 @@ class Md5Pool {
     // time-sliced: a worker that finishes a chunk while chains wait puts its own back at the
     // queue's tail, so every chain advances in turn and the batch ends as one round, not with a
     // tail round of the last few chains (r4ze measured that tail: 64 files on 15 workers)
-    static constexpr int kMaxChains = 4;
+    // (With AVX-512 a worker takes up to 16 chains into the lanes of compress_x16, whose
+    // per-worker throughput keeps rising to 16 chains.)
+    static int max_chains() { return avx512_on() ? 16 : 4; }
     static constexpr size_t kChunk = 256;  // blocks per chain between queue checks
     // The process's CPU share: the cgroup v2 quota where one is set (it is not visible in the
     // affinity mask), else the affinity mask.  Not OMP_NUM_THREADS: launchers such as torchrun
@@ -305,7 +427,7 @@ class Md5Pool {
                     idle_--;
                 }
                 const size_t chains = active_ + q_.size();
-                const size_t share = std::max<size_t>(1, std::min<size_t>(kMaxChains, (chains + workers_ - 1) / workers_));
+                const size_t share = std::max<size_t>(1, std::min<size_t>(max_chains(), (chains + workers_ - 1) / workers_));
                 while (act.size() < share && !q_.empty() && (act.empty() || idle_ == 0)) {
                     act.push_back(q_.front());
                     q_.pop_front();
@@ -314,17 +436,21 @@ class Md5Pool {
             }
             size_t nb = kChunk;
             for (auto *j : act) nb = j->nb < nb ? j->nb : nb;
-            uint32_t *st[kMaxChains];
-            const uint8_t *bp[kMaxChains];
+            uint32_t *st[16];
+            const uint8_t *bp[16];
             for (size_t i = 0; i < act.size(); i++) {
                 st[i] = act[i]->h->h;
                 bp[i] = act[i]->p;
             }
-            switch (act.size()) {
-            case 1: compress_n<1>(st, bp, nb); break;
-            case 2: compress_n<2>(st, bp, nb); break;
-            case 3: compress_n<3>(st, bp, nb); break;
-            default: compress_n<4>(st, bp, nb); break;
+            if (act.size() >= 2 && avx512_on()) {
+                compress_x16(st, bp, (int)act.size(), nb);
+            } else {
+                switch (act.size()) {
+                case 1: compress_n<1>(st, bp, nb); break;
+                case 2: compress_n<2>(st, bp, nb); break;
+                case 3: compress_n<3>(st, bp, nb); break;
+                default: compress_n<4>(st, bp, nb); break;
+                }
             }
             bool finished = false;
             for (auto *j : act) {
@@ -372,12 +498,15 @@ void md5_pool_update_many(HostMd5 *const *hs, const uint8_t *const *data, const 
 
 int md5_pool_workers() { return Md5Pool::get().workers(); }
 
-// Host MD5 rates on this machine: rate[k - 1] = bytes/s per pool worker with k chains each
-// (k = 1..4), measured by running the pool itself on k x workers chains of 256 KiB (one buffer
-// that stays in the caches: the pool's chains stream from memory, but MD5 at ~1 GB/s per chain is
-// far below what a core can fetch), so SMT siblings, the workers' placement and wake-up costs are
-// in the figure; best of three per k, ~3-8 ms in all.  Without a pool: one chain on the caller.
-void md5_measure_rates(double rate[4]) {
+bool md5_avx512() { return avx512_on(); }
+
+// Host MD5 rates on this machine: rate[i] = bytes/s per pool worker with pts[i] chains each
+// (pts = 1, 2, 3, 4 for the scalar interleave; 1, 4, 8, 16 with the AVX-512 path), measured by
+// running the pool itself on pts[i] x workers chains of 256 KiB (one buffer that stays in the
+// caches: the pool's chains stream from memory, but MD5 at ~1 GB/s per chain is far below what a
+// core can fetch), so SMT siblings, the workers' placement and wake-up costs are in the figure;
+// best of three per point, ~5-15 ms in all.  Without a pool: one chain on the caller.
+void md5_measure_rates(double rate[4], uint32_t pts[4]) {
     constexpr size_t kLen = 256 * 1024;
     static uint8_t *buf = [] {
         uint8_t *b = new uint8_t[kLen];
@@ -390,13 +519,15 @@ void md5_measure_rates(double rate[4]) {
     }();
     Md5Pool &pool = Md5Pool::get();
     const int W = pool.workers();
-    for (int k = 1; k <= 4; k++) {
-        const size_t n = W > 0 ? (size_t)k * W : 1;
+    const bool vec = avx512_on();
+    for (int i = 0; i < 4; i++) pts[i] = vec ? (i == 0 ? 1u : 4u << (i - 1)) : (uint32_t)(i + 1);
+    for (int i = 0; i < 4; i++) {
+        const size_t n = W > 0 ? (size_t)pts[i] * W : 1;
         std::vector<HostMd5> hs(n);
         std::vector<HostMd5 *> hp(n);
         std::vector<const uint8_t *> ps(n, buf);
         std::vector<size_t> lens(n, kLen);
-        for (size_t i = 0; i < n; i++) hp[i] = &hs[i];
+        for (size_t j = 0; j < n; j++) hp[j] = &hs[j];
         double best = 0;
         for (int rep = 0; rep < 3; rep++) {
             const auto t0 = std::chrono::steady_clock::now();
@@ -405,7 +536,7 @@ void md5_measure_rates(double rate[4]) {
             const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             if (dt > 0) best = std::max(best, (double)n * kLen / dt / (W > 0 ? W : 1));
         }
-        rate[k - 1] = best;
+        rate[i] = best;
         if (W == 0) {
             for (int j = 1; j < 4; j++) rate[j] = best;
             break;

@@ -21,10 +21,11 @@ struct HostMd5 {
 };
 
 // h->update(data, len) on the process-wide hashing pool (fg_md5_host.cpp): the bulk of a long
-// update runs on a pool worker that hashes up to four callers' messages at once, their chains
-// interleaved step by step (one MD5 chain leaves most of a core's ALU ports idle), so files
-// encoded concurrently hash 2-3x faster per core than one scalar chain each; more chains than
-// 4 x workers are time-sliced.  Blocks until done.
+// update runs on a pool worker that hashes several callers' messages at once -- up to four chains
+// interleaved step by step, or sixteen in the lanes of AVX-512 registers where the host has it
+// (one MD5 chain leaves most of a core's issue width idle) -- so files encoded concurrently hash
+// several times faster per core than one scalar chain each; more chains than fit the workers are
+// time-sliced.  Blocks until done.
 // FLACGPU_MD5_THREADS sets the worker count (default: the process's CPU share -- the cgroup quota,
 // else the affinity mask's CPUs, divided by LOCAL_WORLD_SIZE when a launcher sets it; -1: no
 // pool, each caller hashes its own chain).
@@ -37,8 +38,11 @@ void md5_pool_update_many(HostMd5 *const *hs, const uint8_t *const *data, const 
 // the pool's worker count (0: every caller hashes its own chain)
 int md5_pool_workers();
 
-// measured host MD5 rates: bytes/s per pool worker with k = 1..4 chains each, rate[k - 1]
-// (no pool: one chain's rate on the caller in every entry)
-void md5_measure_rates(double rate[4]);
+// measured host MD5 rates: bytes/s per pool worker with pts[i] chains each (pts: 1, 2, 3, 4; with
+// the AVX-512 path 1, 4, 8, 16); no pool: one chain's rate on the caller in every entry
+void md5_measure_rates(double rate[4], uint32_t pts[4]);
+
+// the AVX-512 sixteen-chain MD5 is in use (host support, FLACGPU_MD5_AVX512 != 0)
+bool md5_avx512();
 
 }  // namespace fg

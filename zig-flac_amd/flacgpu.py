@@ -120,11 +120,11 @@ def md5_many(chunks: Sequence, final: Optional[Sequence[bool]] = None, states=No
 
 class Md5Rates(ctypes.Structure):
     """flacgpu_md5_rates: the rates the MD5 engine choice is priced with (bytes/s)."""
-    _fields_ = [("host_chain", ctypes.c_double * 4), ("device_lane", ctypes.c_double),
+    _fields_ = [("host_chain", ctypes.c_double * 4), ("host_chains", ctypes.c_uint32 * 4), ("device_lane", ctypes.c_double),
                 ("device_chip", ctypes.c_double), ("host_workers", ctypes.c_int32), ("measured", ctypes.c_int32)]
 
     def as_dict(self) -> dict:
-        return {"host_chain": list(self.host_chain), "device_lane": self.device_lane, "device_chip": self.device_chip,
+        return {"host_chain": list(self.host_chain), "host_chains": list(self.host_chains), "device_lane": self.device_lane, "device_chip": self.device_chip,
                 "host_workers": self.host_workers, "measured": self.measured}
 
 
