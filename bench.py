@@ -528,7 +528,8 @@ def end_to_end(args):
             k += 7
         files.append(buf)
     L = flacgpu.load_library()
-    encs = [flacgpu.Encoder(ch, bits, rate, device=0, max_frames=4096) for _ in files]
+    # 6144 frames: three chunk sets of 2048 frames (32 MiB of PCM) for the pipelined schedule
+    encs = [flacgpu.Encoder(ch, bits, rate, device=0, max_frames=6144) for _ in files]
     cap = 200 + ((n + 4095) // 4096 + 1) * encs[0].frame_bound()
     outs = [pinned(cap) for _ in files]
     lens = [ctypes.c_size_t(0) for _ in files]
@@ -583,6 +584,7 @@ def end_to_end(args):
         bt = [batch(nf) for _ in range(2)]
         bbest = min(t for t, _ in bt)
         ok_b = all(rc == 0 for _, rc in bt)
+        out_b = sum(lens[i].value for i in range(nf))
         curve.append({"files": nf, "value": round(nf * n / best / 1e6, 1), "wall_ms": round(best * 1e3, 2),
                       "md5_pool_alone_ms": round(md5_alone * 1e3, 2),
                       "frames_alone_ms": round(frames_alone * 1e3, 2),
@@ -590,7 +592,9 @@ def end_to_end(args):
                       "frac_of_bound": round(bound / best, 3),
                       "binding": "host_md5" if md5_alone >= frames_alone else "gpu_pcie_frames",
                       "batch": {"value": round(nf * n / bbest / 1e6, 1), "wall_ms": round(bbest * 1e3, 2),
-                                "frac_of_md5_bound": round(md5_alone / bbest, 3), "ok": ok_b},
+                                "frac_of_md5_bound": round(md5_alone / bbest, 3), "ok": ok_b,
+                                # the schedule's PCIe traffic: PCM up + frames down over the batch's wall
+                                "h2d_gbs": round(nf * n * fb / bbest / 1e9, 2), "d2h_gbs": round(out_b / bbest / 1e9, 2)},
                       "ok": ok_nf and ok_b})
     ok = all(c["ok"] for c in curve)
     # bounds: one file's MD5 on one host core; pinned H2D bandwidth
@@ -622,7 +626,9 @@ def end_to_end(args):
     runs = [(c["value"], c["files"], c["wall_ms"], "per_file") for c in curve] + \
            [(c["batch"]["value"], c["files"], c["batch"]["wall_ms"], "batch") for c in curve]
     top = max(runs)
+    big = max(curve, key=lambda c: c["files"])
     return {"files": top[1], "mode": top[3], "minutes_per_file": args.e2e_minutes, "samples": top[1] * n,
+            "batch_gbs": [big["batch"]["h2d_gbs"], big["batch"]["d2h_gbs"]],
             "value": top[0], "unit": "MSamples/s", "wall_ms": top[2], "curve": curve,
             "md5_one_file_host_core_ms": round(md5_s * 1e3, 2),
             "bounds_msamples_per_s": {

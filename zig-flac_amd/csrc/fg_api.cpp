@@ -82,6 +82,13 @@ struct TimedLaunch {
 
 }  // namespace
 
+// chunk sets of the pipelined host-buffer path (encode_pipelined): chunk i uploads into set i % 3
+// while chunk i-1 encodes and chunks i-2, i-3 download -- with two sets the upload of chunk i had
+// to wait for the encode of chunk i-2 and the encode for the download of chunk i-2, so a slow
+// download or a late host thread stalled both directions of PCIe (round-4 batches reached 33-44 GB/s
+// of H2D against 57 GB/s measured alone)
+constexpr uint32_t kPipeSets = 3;
+
 struct flacgpu_ctx {
     int device = 0;
     flacgpu_config cfg{};
@@ -93,9 +100,11 @@ struct flacgpu_ctx {
     hipStream_t stream = nullptr, aux = nullptr;
     hipStream_t dl = nullptr;  // download stream of the pipelined host-buffer path
     hipStream_t up = nullptr;  // its upload stream (chunk i+1's upload beside chunk i's encode)
-    hipEvent_t up_done[2] = {nullptr, nullptr};  // a chunk set's upload landed (GPU-side waits)
+    hipEvent_t up_done[kPipeSets] = {};  // a chunk set's upload landed (GPU-side waits)
+    hipEvent_t set_done[kPipeSets] = {};  // a chunk set's encode finished (host waits: blocking sync)
     hipEvent_t fork = nullptr, join = nullptr;
-    // host waits of the pipelined host-buffer path (two chunk sets, the download stream, the end):
+    // host waits of the pipelined host-buffer path (the download stream, the end; the chunk sets'
+    // own events are set_done below):
     // blocking-sync events, so a waiting thread sleeps instead of spinning on a core the MD5 pool
     // and the other files' threads need (FLACGPU_SPIN_SYNC=1: spinning events, A/B)
     hipEvent_t hw[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -779,6 +788,8 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
 #endif
         for (hipEvent_t &ev : c->hw)
             if (hipEventCreateWithFlags(&ev, fl) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+        for (hipEvent_t &ev : c->set_done)
+            if (hipEventCreateWithFlags(&ev, fl) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     }
 
     // CRC-16 shift constants of the table-free fold (mod Q, fg_device.hpp crc_lane_q): thread t
@@ -820,7 +831,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         hipMalloc(&c->d_crc_join, pj.size() * 2) || hipMalloc(&c->d_err, 16) || hipMalloc(&c->d_ctr, 4u * kCtrSet * kOvlMaxChunks) ||
         hipMalloc(&c->d_cum, 8u * (kOvlMaxChunks + 1u)) ||
         hipMalloc(&c->d_jobs, F * sizeof(FrameJob)) || hipMalloc(&c->d_desc, F * (uint64_t)c->desc_stride) ||
-        hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 16) ||
+        hipMalloc(&c->d_fbytes, F * 4) || hipMalloc(&c->d_offsets, F * 8) || hipMalloc(&c->d_total, 8u * (kPipeSets + 1u)) ||
         hipMalloc(&c->d_pcm, c->pcm_cap) || hipMalloc(&c->d_out, c->out_cap) || hipMalloc(&c->d_md5_state, 16) || hipMalloc(&c->d_stamps, 32 * 8))
         return fail(FLACGPU_ERR_OUT_OF_MEMORY);
     if (hipMemcpy(c->d_crc_pow, pw.data(), pw.size() * 2, hipMemcpyHostToDevice) ||
@@ -870,15 +881,17 @@ void flacgpu_close(flacgpu_ctx *c) {
     if (c->up) hipStreamDestroy(c->up);
     for (hipEvent_t e : c->up_done)
         if (e) hipEventDestroy(e);
+    for (hipEvent_t e : c->set_done)
+        if (e) hipEventDestroy(e);
     if (c->ovl) hipStreamDestroy(c->ovl);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
 
 // Host buffers in, host buffers out, with both PCIe directions and the encode overlapped: the
-// context's device buffers split into two halves (chunk sets); chunk i+1 uploads on c->up while
-// chunk i encodes on c->stream and chunk i-1's frames download on c->dl, issued by one worker
-// thread (pageable copies block the issuing thread, so the download needs a thread of its own).
+// context's device buffers split into kPipeSets (3) chunk sets; chunk i+1 uploads on c->up while
+// chunk i encodes on c->stream and the frames of chunks i-1, i-2 download on c->dl, issued by one
+// worker thread (pageable copies block the issuing thread, so the download needs a thread of its own).
 // Output bytes and frame sizes are identical to the sequential loop; only the schedule differs.
 // The input is a list of segments (files, flacgpu_encode_files): chunks never span two, and the
 // pipeline runs on from one segment into the next instead of draining at each file's end.
@@ -897,12 +910,13 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     const uint32_t bs = c->cfg.block_size;
     const uint64_t stride = (uint64_t)bs * c->C * c->B;
     // chunks of at most 2048 frames (32 MiB of 16-bit stereo) so that long inputs keep both
-    // PCIe directions busy; the halves of the context's buffers hold one chunk each
-    const uint64_t F = std::min<uint64_t>(c->max_frames / 2u, 2048u);
-    const uint64_t pcm_half = (uint64_t)(c->max_frames / 2u) * kBlock * c->C * c->B;  // 16-B multiple
-    const uint64_t out_half = (uint64_t)(c->max_frames / 2u) * c->image_bytes;
-    const uint64_t fb_half = c->max_frames / 2u;
-    hipEvent_t *done = c->hw;  // a chunk set's encode finished (blocking-sync events)
+    // PCIe directions busy; the thirds of the context's buffers hold one chunk each
+    const uint64_t part = c->max_frames / kPipeSets;  // frames of one chunk set
+    const uint64_t F = std::min<uint64_t>(part, 2048u);
+    const uint64_t pcm_half = part * kBlock * c->C * c->B;  // 16-B multiple
+    const uint64_t out_half = part * c->image_bytes;
+    const uint64_t fb_half = part;
+    hipEvent_t *done = c->set_done;  // a chunk set's encode finished (blocking-sync events)
     struct Dl {
         int set;
         PipeSeg *sg;
@@ -971,22 +985,22 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
         sg->written = 0;
         const uint64_t total_frames = frames_for(sg->n_samples, bs);
         for (uint64_t frame0 = 0; frame0 < total_frames && rc == FLACGPU_OK; chunk++) {
-            const int set = (int)(chunk & 1u);
+            const int set = (int)(chunk % kPipeSets);
             const uint64_t nf = std::min<uint64_t>(F, total_frames - frame0);
             const uint64_t s0 = frame0 * bs;
             const uint64_t ns = std::min<uint64_t>(nf * bs, sg->n_samples - s0);
             uint8_t *dp = c->d_pcm + set * pcm_half;
-            // upload: the PCM half was last read by chunk i-2's encode (its `done` event, a GPU-side
-            // wait); it runs beside chunk i-1's encode and chunk i-2's download
-            if ((chunk >= 2 && hipStreamWaitEvent(c->up, done[set], 0) != hipSuccess) ||
+            // upload: the PCM part was last read by chunk i-3's encode (its `done` event, a GPU-side
+            // wait); it runs beside chunk i-1's encode and the downloads of chunks i-2, i-3
+            if ((chunk >= kPipeSets && hipStreamWaitEvent(c->up, done[set], 0) != hipSuccess) ||
                 hipMemcpyAsync(dp, sg->src + s0 * c->C * c->B, ns * c->C * c->B, hipMemcpyHostToDevice, c->up) !=
                     hipSuccess ||
                 hipEventRecord(c->up_done[set], c->up) != hipSuccess) {
                 rc = FLACGPU_ERR_DEVICE;
                 break;
             }
-            // the encode writes the output half chunk i-2's download reads: that download first
-            if (chunk >= 2 && (rc = wait_done(chunk - 1))) break;
+            // the encode writes the output part chunk i-3's download reads: that download first
+            if (chunk >= kPipeSets && (rc = wait_done(chunk - kPipeSets + 1))) break;
             if (hipStreamWaitEvent(c->stream, c->up_done[set], 0) != hipSuccess ||
                 launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, sg->first_frame_number + frame0, (uint32_t)nf,
                                  c->stream) != hipSuccess) {
@@ -1044,7 +1058,7 @@ int fg::ctx_encode_segments(flacgpu_ctx *c, uint32_t n, const uint8_t *const *sr
         }
         return FLACGPU_OK;
     };
-    if (c->max_frames < 2 || c->records_on) return one_by_one();
+    if (c->max_frames < kPipeSets || c->records_on) return one_by_one();
     std::vector<PipeSeg> segs;
     try {
         segs.resize(n);
@@ -1082,7 +1096,7 @@ int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sa
     uint64_t frame0 = 0;
     size_t written = 0;
     if (c->records_on) c->h_records.clear();
-    if (!c->records_on && c->max_frames >= 2 && total_frames > std::min<uint64_t>(c->max_frames / 2u, 2048u)) {
+    if (!c->records_on && c->max_frames >= kPipeSets && total_frames > std::min<uint64_t>(c->max_frames / kPipeSets, 2048u)) {
         PipeSeg seg{src, n_samples, first_frame_number, out, out_cap, 0, frame_bytes};
         const int rc = encode_pipelined(c, &seg, 1);
         if (rc != kNoWorker) {

@@ -368,9 +368,13 @@ class Md5Pool {
     // time-sliced: a worker that finishes a chunk while chains wait puts its own back at the
     // queue's tail, so every chain advances in turn and the batch ends as one round, not with a
     // tail round of the last few chains (r4ze measured that tail: 64 files on 15 workers)
-    // (With AVX-512 a worker takes up to 16 chains into the lanes of compress_x16, whose
-    // per-worker throughput keeps rising to 16 chains.)
-    static int max_chains() { return avx512_on() ? 16 : 4; }
+    // With AVX-512 a worker whose share is kVecMin or more chains takes up to 16 into the lanes of
+    // compress_x16, whose per-worker throughput keeps rising to 16 chains; below that the scalar
+    // interleave is faster per chain (EPYC 9575F, r5i: one vector chain 0.42 GB/s, scalar 0.78;
+    // per worker at 4 chains 1.71 vector vs 2.30 scalar GB/s, at 16 chains 6.8 vector vs 2.30
+    // time-sliced scalar)
+    static constexpr size_t kVecMin = 6;
+    static size_t max_chains(size_t share) { return (avx512_on() && share >= kVecMin) ? 16 : 4; }
     static constexpr size_t kChunk = 256;  // blocks per chain between queue checks
     // The process's CPU share: the cgroup v2 quota where one is set (it is not visible in the
     // affinity mask), else the affinity mask.  Not OMP_NUM_THREADS: launchers such as torchrun
@@ -427,7 +431,8 @@ class Md5Pool {
                     idle_--;
                 }
                 const size_t chains = active_ + q_.size();
-                const size_t share = std::max<size_t>(1, std::min<size_t>(max_chains(), (chains + workers_ - 1) / workers_));
+                const size_t even = std::max<size_t>(1, (chains + workers_ - 1) / workers_);
+                const size_t share = std::min<size_t>(max_chains(even), even);
                 while (act.size() < share && !q_.empty() && (act.empty() || idle_ == 0)) {
                     act.push_back(q_.front());
                     q_.pop_front();
@@ -442,7 +447,7 @@ class Md5Pool {
                 st[i] = act[i]->h->h;
                 bp[i] = act[i]->p;
             }
-            if (act.size() >= 2 && avx512_on()) {
+            if (act.size() > 4) {  // only taken with the AVX-512 path (max_chains)
                 compress_x16(st, bp, (int)act.size(), nb);
             } else {
                 switch (act.size()) {
@@ -519,7 +524,7 @@ void md5_measure_rates(double rate[4], uint32_t pts[4]) {
     }();
     Md5Pool &pool = Md5Pool::get();
     const int W = pool.workers();
-    const bool vec = avx512_on();
+    const bool vec = avx512_on();  // points past four chains per worker use the vector path
     for (int i = 0; i < 4; i++) pts[i] = vec ? (i == 0 ? 1u : 4u << (i - 1)) : (uint32_t)(i + 1);
     for (int i = 0; i < 4; i++) {
         const size_t n = W > 0 ? (size_t)pts[i] * W : 1;
