@@ -107,6 +107,9 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-files", default="8,16,32,64", help="file counts of the end-to-end curve")
     p.add_argument("--e2e-minutes", type=float, default=10.0)
+    p.add_argument("--e2e-numa", choices=["local", "off"], default="local",
+                   help="local: every thread of the process on the GPU's NUMA node before the e2e buffers "
+                        "are allocated (pinned pages and the MD5 pool's reads on the GPU's side of the fabric)")
     p.add_argument("--no-sharded", action="store_true", help="skip the sharded single-stream line")
     p.add_argument("--sharded-config", choices=sorted(PRESETS), default="c4")
     p.add_argument("--sharded-frames", type=int, default=8192, help="frames per rank per window (sharded mode)")
@@ -493,6 +496,34 @@ def _timed(fn):
     return time.perf_counter() - t0
 
 
+def gpu_local_cpus():
+    """CPUs of the GPU's NUMA node (sysfs local_cpulist of cuda:0's PCI device) that this process may
+    use, or None."""
+    import torch
+
+    try:
+        pr = torch.cuda.get_device_properties(0)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        txt = open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip()
+        cpus = set()
+        for part in txt.split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        return sorted(cpus) or None
+    except Exception:
+        return None
+
+
+def move_process(cpus):
+    """Every thread of this process onto `cpus` (sched_setaffinity acts per thread)."""
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            os.sched_setaffinity(int(tid), cpus)
+        except OSError:
+            pass
+
+
 def end_to_end(args):
     """BASELINE.md end-to-end contract: host PCM buffers -> .flac files in host memory, as a curve
     over the number of files encoded at once, per file (one context + host thread each) and as one
@@ -508,6 +539,10 @@ def end_to_end(args):
     n = int(args.e2e_minutes * 60 * rate)
     fb = ch * 2
     counts = sorted({int(x) for x in str(args.e2e_files).split(",") if x})
+    saved_aff = os.sched_getaffinity(0)
+    local = gpu_local_cpus() if args.e2e_numa == "local" else None
+    if local:
+        move_process(local)  # before the buffers are allocated and first touched
     nmax = max(counts)
     pool_n = 4096 * 1024
     pool = np.frombuffer(synth.to_pcm_bytes(synth.synth_samples(pool_n, ch, bits, rate, stream=11), bits),
@@ -623,6 +658,8 @@ def end_to_end(args):
     ok &= rcs[0] == 0 and outs[0][: lens[0].value].tobytes() == ref  # and the per-file call's
     for e in encs:
         e.close()
+    if local:
+        move_process(saved_aff)
     runs = [(c["value"], c["files"], c["wall_ms"], "per_file") for c in curve] + \
            [(c["batch"]["value"], c["files"], c["batch"]["wall_ms"], "batch") for c in curve]
     top = max(runs)
@@ -641,6 +678,7 @@ def end_to_end(args):
                     "2048-frame chunks running on from file to file); every file's MD5 on the library's host "
                     "hashing pool beside the encode (up to 8 chains interleaved per core, fg_md5_host.cpp)",
             "md5_pool_threads": os.environ.get("FLACGPU_MD5_THREADS", "default (CPUs of the affinity mask)"),
+            "numa": {"mode": args.e2e_numa, "gpu_local_cpus": len(local) if local else None},
             "output_ok": bool(ok)}
 
 

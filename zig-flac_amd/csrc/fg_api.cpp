@@ -87,7 +87,7 @@ struct TimedLaunch {
 // to wait for the encode of chunk i-2 and the encode for the download of chunk i-2, so a slow
 // download or a late host thread stalled both directions of PCIe (round-4 batches reached 33-44 GB/s
 // of H2D against 57 GB/s measured alone)
-constexpr uint32_t kPipeSets = 3;
+constexpr uint32_t kPipeSets = 3;  // the most; flacgpu_ctx::pipe_sets is the number in use (2 or 3)
 
 struct flacgpu_ctx {
     int device = 0;
@@ -101,7 +101,9 @@ struct flacgpu_ctx {
     hipStream_t dl = nullptr;  // download stream of the pipelined host-buffer path
     hipStream_t up = nullptr;  // its upload stream (chunk i+1's upload beside chunk i's encode)
     hipEvent_t up_done[kPipeSets] = {};  // a chunk set's upload landed (GPU-side waits)
-    hipEvent_t set_done[kPipeSets] = {};  // a chunk set's encode finished (host waits: blocking sync)
+    hipEvent_t set_done[kPipeSets] = {};  // a chunk set's encode finished (GPU-side waits)
+    hipEvent_t dl_done[kPipeSets] = {};   // a chunk set's frames downloaded (GPU-side waits)
+    uint32_t pipe_sets = kPipeSets;  // chunk sets in use (FLACGPU_PIPE_SETS = 2: the round-4 schedule)
     hipEvent_t fork = nullptr, join = nullptr;
     // host waits of the pipelined host-buffer path (the download stream, the end; the chunk sets'
     // own events are set_done below):
@@ -693,6 +695,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (const char *e = std::getenv("FLACGPU_XCD_QUEUE")) c->xcd_queue = e[0] != '0';
     if (const char *e = std::getenv("FLACGPU_PACK_XCDQ")) c->pack_xcdq = e[0] != '0';
     if (const char *e = std::getenv("FLACGPU_SPLIT_JIT")) c->split_jit = (uint32_t)std::atoi(e) & 3u;
+    if (const char *e = std::getenv("FLACGPU_PIPE_SETS")) c->pipe_sets = e[0] == '2' ? 2u : kPipeSets;
 #if FG_DIAG
     // diagnostic build only: issue priorities, grid reserves, the overlapped schedule's shape
     if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);
@@ -789,7 +792,9 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         for (hipEvent_t &ev : c->hw)
             if (hipEventCreateWithFlags(&ev, fl) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
         for (hipEvent_t &ev : c->set_done)
-            if (hipEventCreateWithFlags(&ev, fl) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
+        for (hipEvent_t &ev : c->dl_done)
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(FLACGPU_ERR_DEVICE);
     }
 
     // CRC-16 shift constants of the table-free fold (mod Q, fg_device.hpp crc_lane_q): thread t
@@ -883,6 +888,8 @@ void flacgpu_close(flacgpu_ctx *c) {
         if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->set_done)
         if (e) hipEventDestroy(e);
+    for (hipEvent_t e : c->dl_done)
+        if (e) hipEventDestroy(e);
     if (c->ovl) hipStreamDestroy(c->ovl);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -911,12 +918,13 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     const uint64_t stride = (uint64_t)bs * c->C * c->B;
     // chunks of at most 2048 frames (32 MiB of 16-bit stereo) so that long inputs keep both
     // PCIe directions busy; the thirds of the context's buffers hold one chunk each
-    const uint64_t part = c->max_frames / kPipeSets;  // frames of one chunk set
+    const uint32_t NS = c->pipe_sets;
+    const uint64_t part = c->max_frames / NS;  // frames of one chunk set
     const uint64_t F = std::min<uint64_t>(part, 2048u);
     const uint64_t pcm_half = part * kBlock * c->C * c->B;  // 16-B multiple
     const uint64_t out_half = part * c->image_bytes;
     const uint64_t fb_half = part;
-    hipEvent_t *done = c->set_done;  // a chunk set's encode finished (blocking-sync events)
+    hipEvent_t *done = c->set_done;  // a chunk set's encode finished
     struct Dl {
         int set;
         PipeSeg *sg;
@@ -926,15 +934,19 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     std::mutex m;
     std::condition_variable cv;
     std::deque<Dl> q;
-    uint64_t n_done = 0;  // downloads finished (in chunk order)
+    uint64_t n_done = 0;  // downloads issued (in chunk order; dl_done[set] marks their completion)
     bool closing = false;
     int wrc = FLACGPU_OK;  // the first download error
+    // One host wait per chunk: the download stream waits for the chunk's encode on the GPU, the
+    // worker reads the chunk's byte count (it places the next chunk of the segment), then issues
+    // the copies and records dl_done[set], on which the next encode into that set waits GPU-side.
+    // (Round 4 slept on three blocking-sync events per chunk -- encode done, count, copies done --
+    // and the 64-file batch moved 33 GB/s of PCM against 56 GB/s of chunked H2D beside D2H.)
     auto download = [&](const Dl &d) -> int {
         PipeSeg *sg = d.sg;
-        if (hipSetDevice(c->device) != hipSuccess || hipEventSynchronize(done[d.set]) != hipSuccess)
-            return FLACGPU_ERR_DEVICE;
         uint64_t total = 0;
-        if (hipMemcpyAsync(&total, c->d_total + d.set, 8, hipMemcpyDeviceToHost, c->dl) != hipSuccess ||
+        if (hipSetDevice(c->device) != hipSuccess || hipStreamWaitEvent(c->dl, done[d.set], 0) != hipSuccess ||
+            hipMemcpyAsync(&total, c->d_total + d.set, 8, hipMemcpyDeviceToHost, c->dl) != hipSuccess ||
             wait_host(c, c->dl, 2) != hipSuccess)
             return FLACGPU_ERR_DEVICE;
         if (sg->written + total > sg->out_cap) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
@@ -942,7 +954,7 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
                                                hipMemcpyDeviceToHost, c->dl) != hipSuccess) ||
             hipMemcpyAsync(sg->out + sg->written, c->d_out + d.set * out_half, total, hipMemcpyDeviceToHost, c->dl) !=
                 hipSuccess ||
-            wait_host(c, c->dl, 2) != hipSuccess)
+            hipEventRecord(c->dl_done[d.set], c->dl) != hipSuccess)
             return FLACGPU_ERR_DEVICE;
         sg->written += total;
         return FLACGPU_OK;
@@ -972,7 +984,7 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     } catch (const std::system_error &) {
         return kNoWorker;  // the caller encodes chunk by chunk on this thread instead
     }
-    // wait (host) until at least `k` downloads have finished; the first download error
+    // wait (host) until at least `k` downloads have been issued; the first download error
     auto wait_done = [&](uint64_t k) -> int {
         std::unique_lock<std::mutex> lk(m);
         cv.wait(lk, [&] { return n_done >= k || wrc != FLACGPU_OK; });
@@ -985,14 +997,14 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
         sg->written = 0;
         const uint64_t total_frames = frames_for(sg->n_samples, bs);
         for (uint64_t frame0 = 0; frame0 < total_frames && rc == FLACGPU_OK; chunk++) {
-            const int set = (int)(chunk % kPipeSets);
+            const int set = (int)(chunk % NS);
             const uint64_t nf = std::min<uint64_t>(F, total_frames - frame0);
             const uint64_t s0 = frame0 * bs;
             const uint64_t ns = std::min<uint64_t>(nf * bs, sg->n_samples - s0);
             uint8_t *dp = c->d_pcm + set * pcm_half;
             // upload: the PCM part was last read by chunk i-3's encode (its `done` event, a GPU-side
             // wait); it runs beside chunk i-1's encode and the downloads of chunks i-2, i-3
-            if ((chunk >= kPipeSets && hipStreamWaitEvent(c->up, done[set], 0) != hipSuccess) ||
+            if ((chunk >= NS && hipStreamWaitEvent(c->up, done[set], 0) != hipSuccess) ||
                 hipMemcpyAsync(dp, sg->src + s0 * c->C * c->B, ns * c->C * c->B, hipMemcpyHostToDevice, c->up) !=
                     hipSuccess ||
                 hipEventRecord(c->up_done[set], c->up) != hipSuccess) {
@@ -1000,8 +1012,10 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
                 break;
             }
             // the encode writes the output part chunk i-3's download reads: that download first
-            if (chunk >= kPipeSets && (rc = wait_done(chunk - kPipeSets + 1))) break;
-            if (hipStreamWaitEvent(c->stream, c->up_done[set], 0) != hipSuccess ||
+            // (issued by the worker: then the encode stream waits for its copies on the GPU)
+            if (chunk >= NS && (rc = wait_done(chunk - NS + 1))) break;
+            if ((chunk >= NS && hipStreamWaitEvent(c->stream, c->dl_done[set], 0) != hipSuccess) ||
+                hipStreamWaitEvent(c->stream, c->up_done[set], 0) != hipSuccess ||
                 launch_make_jobs(c->d_jobs, ns, bs, (uint32_t)stride, sg->first_frame_number + frame0, (uint32_t)nf,
                                  c->stream) != hipSuccess) {
                 rc = FLACGPU_ERR_DEVICE;
@@ -1030,6 +1044,8 @@ static int encode_pipelined(flacgpu_ctx *c, PipeSeg *segs, size_t nseg) {
     cv.notify_all();
     worker.join();
     if (rc == FLACGPU_OK) rc = wrc;
+    const hipError_t se = hipStreamSynchronize(c->dl);  // the last chunks' copies
+    if (rc == FLACGPU_OK && se != hipSuccess) rc = FLACGPU_ERR_DEVICE;
     if (rc) {
         hipStreamSynchronize(c->up);
         hipStreamSynchronize(c->stream);
@@ -1058,7 +1074,7 @@ int fg::ctx_encode_segments(flacgpu_ctx *c, uint32_t n, const uint8_t *const *sr
         }
         return FLACGPU_OK;
     };
-    if (c->max_frames < kPipeSets || c->records_on) return one_by_one();
+    if (c->max_frames < c->pipe_sets || c->records_on) return one_by_one();
     std::vector<PipeSeg> segs;
     try {
         segs.resize(n);
@@ -1096,7 +1112,8 @@ int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sa
     uint64_t frame0 = 0;
     size_t written = 0;
     if (c->records_on) c->h_records.clear();
-    if (!c->records_on && c->max_frames >= kPipeSets && total_frames > std::min<uint64_t>(c->max_frames / kPipeSets, 2048u)) {
+    if (!c->records_on && c->max_frames >= c->pipe_sets &&
+        total_frames > std::min<uint64_t>(c->max_frames / c->pipe_sets, 2048u)) {
         PipeSeg seg{src, n_samples, first_frame_number, out, out_cap, 0, frame_bytes};
         const int rc = encode_pipelined(c, &seg, 1);
         if (rc != kNoWorker) {
