@@ -156,6 +156,23 @@ def test_gpu_encode_files_without_md5_diagnostic(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sets", ["2", "3"])
+def test_gpu_encode_files_pipe_sets(sets, monkeypatch):
+    """The pipelined schedule with two or three chunk sets (FLACGPU_PIPE_SETS, output-invariant):
+    files several chunks long (6-frame chunks), ragged and empty, byte-identical to the oracle."""
+    monkeypatch.setenv("FLACGPU_PIPE_SETS", sets)
+    ch, bits, rate = 2, 16, 44100
+    lens = [40 * 4096 + 333, 0, 13 * 4096, 7 * 4096 + 1]
+    pcms = [synth.synth_pcm(n, ch, bits, rate, stream=80 + i) if n else b"" for i, n in enumerate(lens)]
+    with flacgpu.Encoder(ch, bits, rate, max_frames=18) as enc:
+        outs = enc.encode_files(pcms)
+        one = enc.encode_file(pcms[0])
+    for i, pcm in enumerate(pcms):
+        assert outs[i] == oracle_ref.encode_file(pcm, ch, bits, rate), f"file {i}"
+    assert one == outs[0]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["max_frames_1", "records_on"])
 def test_gpu_encode_files_where_the_pipeline_cannot_run(mode):
     """flacgpu_encode_files on the contexts its pipelined schedule cannot serve (one frame per call;
