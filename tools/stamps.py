@@ -10,7 +10,7 @@ NAMES = ["DMA issue+job load", "sample load", "waste+eq", "bestOrder", "rice pas
          "fixed rice search", "LPC load+autocorr", "LPC Levinson-Durbin", "LPC residual pass"]
 PNAMES = ["top barrier", "offsets+bar", "zero img+bars", "residuals", "pack codes+bar", "CRC+bars", "store+bar",
           "ticket+desc loads", "vmcnt(0) wait", "DMA issue+sample load", "lane_bits/bits loads+scan"]
-S, F = 1024, 32
+S, F = int(os.environ.get("STAMP_S", "1024")), int(os.environ.get("STAMP_F", "32"))
 CH, BITS, RATE = int(os.environ.get("CH", "2")), int(os.environ.get("BITS", "16")), int(os.environ.get("RATE", "44100"))
 FB = CH * BITS // 8
 LPC = int(os.environ.get("LPC", "0"))

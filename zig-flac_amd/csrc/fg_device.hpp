@@ -496,6 +496,15 @@ struct CandRes {
     int32_t lsh;  // LPC quantisation shift
     uint64_t est;
     int64_t cval;
+    // every field is wave-uniform: pinned to SGPRs (readfirstlane) before the LPC search, whose
+    // register peak otherwise spilled the VGPR copies the merges of divergent-looking control flow
+    // had made of them (c3: 12 dwords of scratch stores per lane and frame)
+    __device__ __forceinline__ void make_uniform() {
+        auto u32 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+        auto u64 = [&](uint64_t v) { return (uint64_t)u32((uint32_t)v) | ((uint64_t)u32((uint32_t)(v >> 32)) << 32); };
+        type = u32(type); waste = u32(waste); bd = u32(bd); order = u32(order); porder = u32(porder);
+        method = u32(method); lsh = (int32_t)u32((uint32_t)lsh); est = u64(est); cval = (int64_t)u64((uint64_t)cval);
+    }
 };
 
 #ifdef FG_STAMPS
@@ -1934,6 +1943,7 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
             // usable coefficients; total = rice + q (bps' + 15) + 9; strictly smaller replaces
             ltab = (int32_t *)(smem + LY.lpc) + wave * (uint32_t)kLpcTab;
             const uint32_t Q = a.lpc_order;
+            R.make_uniform();
             if (lpc_on && R.type != 0 && n > Q) {
                 STAMP(11);  // (stamps build: the fixed predictor's search ends here)
                 bool fits;
