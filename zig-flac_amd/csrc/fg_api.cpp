@@ -727,13 +727,13 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
         uint32_t wps = n_out <= 4u ? 4u : 2u;
         if (const char *e = std::getenv("FLACGPU_PACKW_WPS")) wps = (e[0] == '2' && n_out <= 8u) ? 2u : wps;  // tuning knob
         c->nt_pack4 = 64u * n_out * wps;
-        packw_dbuf = packw_layout(c->C, c->B, wps, c->image_bytes, true).total * 2u <= 160u * 1024u;
+        packw_dbuf = packw_layout(c->C, c->B, wps, c->image_bytes, true, n_out).total * 2u <= 160u * 1024u;
         if (const char *e = std::getenv("FLACGPU_PACKW_DBUF")) packw_dbuf = packw_dbuf && e[0] == '1';  // tuning knob
         c->pack_dbuf = packw_dbuf;  // k_pack then runs tail frames only (never double-buffered)
     }
     if (c->nt_pack4) {
         c->lds_pack4 = (c->C == 2 && c->B == 2 && !lpc) ? pack4_layout(c->image_bytes).total
-                                                         : packw_layout(c->C, c->B, c->nt_pack4 / (64u * n_out), c->image_bytes, packw_dbuf).total;
+                                                         : packw_layout(c->C, c->B, c->nt_pack4 / (64u * n_out), c->image_bytes, packw_dbuf, n_out).total;
         c->crc_hmax4 = ((c->image_bytes / 4u + 2u * c->nt_pack4 - 1u) / (2u * c->nt_pack4)) | 1u;
     }
     // Frames whose single-buffered k_packw staging admits one workgroup per CU and whose analysis
@@ -741,7 +741,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (c->ana_split && use_packw && !packw_dbuf) {
         const uint32_t ch = c->C / 2u;
         const uint32_t img = fg_round16(frame_bound_bytes(kBlock, ch, c->bits, false) + 16u);
-        const uint32_t lh = packw_layout(ch, c->B, 2u, img, false).total;
+        const uint32_t lh = packw_layout(ch, c->B, 2u, img, false, ch).total;
         bool on = 2u * lh <= 160u * 1024u;
         if (const char *e = std::getenv("FLACGPU_PACK_SPLIT")) on = on && e[0] != '0';  // A/B knob
         if (on) {

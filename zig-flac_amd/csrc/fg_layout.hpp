@@ -26,8 +26,8 @@ struct AnaLayout {
 struct PackLayout {
     uint32_t buf0;   // PCM staging of a frame, then (aliasing it) the frame image (big-endian words)
     uint32_t buf1;   // second buffer: the next frame's PCM arrives by LDS-DMA (== buf0 without)
-    uint32_t crc;    // 8 x 256 u16 CRC tables
     uint32_t misc;   // 64 x u32 scratch (crc partials)
+    uint32_t dsc;    // k_packw: two LDS copies of a frame descriptor's fields (packw_dsc_dw each)
     uint32_t total;
 };
 
@@ -90,9 +90,9 @@ __host__ __device__ inline PackLayout pack_layout(uint32_t C, uint32_t B, uint32
     L.buf0 = 0;
     L.buf1 = dbuf ? r0 : 0u;
     // (until round 5 a 4-KiB CRC table area sat here; the table-free CRC of round 3 left it unused)
-    L.crc = dbuf ? 2u * r0 : r0;
-    L.misc = L.crc;
-    L.total = fg_round16(L.misc + 256u);
+    L.misc = dbuf ? 2u * r0 : r0;
+    L.dsc = L.misc + 256u;
+    L.total = fg_round16(L.dsc);
     return L;
 }
 
@@ -127,7 +127,14 @@ __host__ __device__ inline P4Layout pack4_layout(uint32_t image_bytes) {
 // one chunk start in different banks (with the plain pad they would all hit one: a sub-chunk of
 // 16 or 32 samples is a multiple of 32 words for 8-byte and 24-byte sample rows).
 __host__ __device__ inline uint32_t packw_cst(uint32_t C, uint32_t B, uint32_t wps) { return 16u * C * B + wps; }
-__host__ __device__ inline PackLayout packw_layout(uint32_t C, uint32_t B, uint32_t wps, uint32_t image_bytes, bool dbuf) {
+// k_packw's LDS copy of a frame descriptor (fg_packw.hpp, dsc_dma) for nh written subframes per
+// workgroup: hc header chunks of 64 dwords (frame fields, the subframes' bit counts, the frame's
+// offset, 11 fields per local subframe), then nh chunks of lane bit counts and nh of Rice
+// parameters
+__host__ __device__ inline uint32_t packw_dsc_hc(uint32_t nh) { return (18u + 11u * nh + 63u) / 64u; }
+__host__ __device__ inline uint32_t packw_dsc_dw(uint32_t nh) { return 64u * (packw_dsc_hc(nh) + 2u * nh); }
+__host__ __device__ inline PackLayout packw_layout(uint32_t C, uint32_t B, uint32_t wps, uint32_t image_bytes, bool dbuf,
+                                                   uint32_t nh) {
     PackLayout L;
     uint32_t r0 = 64u * packw_cst(C, B, wps) * 4u;
     if (image_bytes > r0) r0 = image_bytes;
@@ -135,9 +142,9 @@ __host__ __device__ inline PackLayout packw_layout(uint32_t C, uint32_t B, uint3
     L.buf0 = 0;
     L.buf1 = dbuf ? r0 : 0u;
     // (until round 5 a 4-KiB CRC table area sat here; the table-free CRC of round 3 left it unused)
-    L.crc = dbuf ? 2u * r0 : r0;
-    L.misc = L.crc;
-    L.total = fg_round16(L.misc + 256u);
+    L.misc = dbuf ? 2u * r0 : r0;
+    L.dsc = L.misc + 256u;
+    L.total = fg_round16(L.dsc + 2u * 4u * packw_dsc_dw(nh));
     return L;
 }
 

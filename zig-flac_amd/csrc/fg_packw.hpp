@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     const uint32_t cw = 16u * C * B, cst = packw_cst(C, B, WPS);
     const uint32_t sw = (uint32_t)SPL * CB / 4u;  // words of one lane's sub-chunk
     const bool dbuf = a.pack_dbuf != 0;
-    const PackLayout LY = packw_layout(C, B, WPS, a.image_bytes, dbuf);
+    const PackLayout LY = packw_layout(C, B, WPS, a.image_bytes, dbuf, NW / WPS);
     uint32_t dcode = 0;  // per lane, 3 bits per DMA slot (cst <= 516 words: 9 slots)
 #pragma unroll
     for (uint32_t xi = 0; xi < 9u; xi++) {
@@ -144,6 +144,43 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
     if (nxt < n_items) jn = a.jobs[nxt >> ssh];
     if (dbuf && jidx < n_items)
         stage_dma_w(a.pcm, job.pcm_off, (uint32_t *)(smem + LY.buf0), cw, cst, dcode, wave, NW, l0, drh, jidx & ssh);
+    // The frame descriptor's fields this workgroup reads, in LDS (two slots, packw_dsc_dw): one
+    // frame's copy is DMA'd during the frame before it, so the top of a frame reads them from LDS
+    // instead of running dependent global round trips to the table the analysis kernel wrote (the
+    // subframes' bit counts -> their prefix -> the image size -> the CRC constants: 28 % of a c4
+    // pack wave's time in r5q's stamps).  Dwords: [0..7] FrameDesc, [8..15] SubDesc.bits of the
+    // frame's subframes, [16..17] the frame's byte offset, then 11 per local subframe (SubDesc
+    // dwords 0, 1, 3, 4, 5, 134..139: fields, lpc_prec, cval, coef); chunk HC + s: lane_bits of
+    // local subframe s; chunk HC + NH + s: its Rice parameters.
+    const uint32_t HC = packw_dsc_hc(NH), DSC_DW = packw_dsc_dw(NH);
+    uint32_t *dscb = (uint32_t *)(smem + LY.dsc);
+    auto dsc_dma = [&](uint32_t fslot, uint32_t hf, uint32_t ds) {
+        const uint8_t *fdp = a.desc + (uint64_t)fslot * a.desc_stride;
+        uint32_t *dst = dscb + ds * DSC_DW;
+        const uint32_t nsubx = NH << ssh;
+        const uint32_t ll = opaque(l0);
+        for (uint32_t kc = wave; kc < HC + 2u * NH; kc += NW) {
+            const uint8_t *src = fdp;
+            if (kc < HC) {
+                const uint32_t q = 64u * kc + ll;
+                if (q < 8u) src = fdp + 4u * q;
+                else if (q < 16u) src = (q - 8u < nsubx) ? fdp + 32u + (q - 8u) * (uint32_t)sizeof(SubDesc) + 8u : fdp;
+                else if (q < 18u) src = (const uint8_t *)(a.offsets + fslot) + 4u * (q - 16u);
+                else if (q < 18u + 11u * NH) {
+                    const uint32_t sl = (q - 18u) / 11u, f = (q - 18u) - 11u * sl;
+                    const uint32_t dw = f < 2u ? f : (f == 2u ? 3u : (f < 5u ? f + 1u : 129u + f));
+                    src = fdp + 32u + (hf * NH + sl) * (uint32_t)sizeof(SubDesc) + 4u * dw;
+                }
+            } else if (kc < HC + NH) {
+                src = fdp + 32u + (hf * NH + (kc - HC)) * (uint32_t)sizeof(SubDesc) + 24u + 4u * ll;
+            } else {
+                src = fdp + 32u + (hf * NH + (kc - HC - NH)) * (uint32_t)sizeof(SubDesc) + 280u + 4u * ll;
+            }
+            lds_dma<4>(src, dst + 64u * kc);
+        }
+    };
+    uint32_t dslot = 0;      // the LDS slot holding (or receiving) the current frame's descriptor
+    bool dsc_ready = false;  // it was DMA'd during the previous frame
 #ifdef FG_STAMPS
     uint64_t ph_[16] = {};
     uint64_t tprev_ = __builtin_amdgcn_s_memtime();
@@ -157,24 +194,30 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         // single buffer: the frame's DMA first, so the descriptor's dependent loads below run
         // under it instead of ahead of it (the previous frame's last barrier freed the buffer)
         if (!dbuf) stage_dma_w(a.pcm, job.pcm_off, stg, cw, cst, dcode, wave, NW, l, drh, half);
-        const uint8_t *fd = a.desc + (uint64_t)job.slot * a.desc_stride;
-        const FrameDesc *F = (const FrameDesc *)fd;
-        const SubDesc *sd0 = (const SubDesc *)(fd + sizeof(FrameDesc));
+        if (!dsc_ready) dsc_dma(job.slot, half, dslot);  // (first frame, or jit: no look-ahead)
+        const uint32_t *dsc = dscb + dslot * DSC_DW;
+
+        // ---- 1. PCM (double-buffered: DMA'd during the previous frame) -> samples
+        STAMP(7);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(8);
+        __syncthreads();
+        STAMP(0);
         const uint32_t sidx = half * NH + sfi;  // this wave's subframe in the frame
-        const SubDesc *sd = sd0 + sidx;
-        const uint32_t total_bits = F->total_bits;
+        const uint32_t *sdh = dsc + 18u + 11u * sfi;  // its fields (see dsc_dma)
+        const uint32_t hdr_bytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[0]);
+        const uint32_t total_bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[1]);
+        const uint32_t n_out_f = (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[3]);
         const uint32_t Lt = (total_bits + 7u) >> 3;  // the frame's bytes before the CRC
-        const uint64_t D = a.offsets[job.slot];
+        const uint64_t D = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[17]) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)dsc[16]);
         // split: half 0 ends at bit b0 (header + its subframes); half 1's image starts at byte
         // b0 / 8 and ends with the frame.  Lb = this image's bytes (whole frame: Lt)
-        // every subframe's bits in one load (lane t: subframe t), summed below by readlanes: the
-        // loop over sd0[t].bits was a chain of dependent descriptor reads (r3g stamps: 32 % of a
-        // c4 pack wave's time in the descriptor loads)
         const uint32_t nsub = NH << ssh;
-        const uint32_t sbits = l < nsub ? sd0[l].bits : 0u;
+        const uint32_t sbits = l < nsub ? dsc[8u + l] : 0u;
         uint32_t b0 = 0, base = 0, Lb = Lt;
         if (SPLIT) {
-            b0 = 8u * F->hdr_bytes;
+            b0 = 8u * hdr_bytes;
             for (uint32_t t = 0; t < NH; t++) b0 += rdl(sbits, (int)t);
             base = half ? (b0 >> 3) : 0u;
             Lb = half ? Lt - base : (b0 + 7u) >> 3;
@@ -183,30 +226,38 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         const uint32_t W4 = Lb >> 2;
         const uint32_t H = max((W4 + 2u * NT - 1u) / (2u * NT), 1u);  // words per thread / 2
         const uint32_t hcq = min(H, a.crc_hmax4) - 1u;
-        const uint32_t crc_pw = a.crc_pow4[hcq * NT + tid];
+        const uint32_t crc_pw = a.crc_pow4[hcq * NT + tid];  // first used in the CRC phase
         const bool skip = fbytes + 16u > a.image_bytes || D + Lt + 2u > a.out_cap;  // uniform
-        const uint32_t type = sd->type, w = sd->waste, bd = sd->bd, k = sd->order, o = sd->porder,
-                       method = sd->method, cand = sd->cand;
+        const uint32_t sw0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sdh[0]),
+                       sw1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sdh[1]);
+        const uint32_t type = sw0 & 255u, w = (sw0 >> 8) & 255u, bd = (sw0 >> 16) & 255u, k = sw0 >> 24,
+                       o = sw1 & 255u, method = (sw1 >> 8) & 255u, cand = (sw1 >> 16) & 255u;
+        const int32_t lpc_shift = (int32_t)(int8_t)(sw1 >> 24);
+        const uint32_t lpc_prec = (uint32_t)__builtin_amdgcn_readfirstlane((int)sdh[2]);
+        const int64_t cval = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)sdh[4]) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)sdh[3]));
+        const uint16_t *coef = (const uint16_t *)(sdh + 5);
         const uint32_t i0 = hq * 64u * SPL + SPL * l0;  // first sample of this lane
         uint32_t pq[NG];
+        const uint8_t *prm = (const uint8_t *)(dsc + 64u * (HC + NH + sfi));
 #pragma unroll
-        for (int g = 0; g < NG; g++) pq[g] = sd->params[(i0 + 16u * g) >> (12u - o)];
-        const uint32_t lb = sd->lane_bits[l0];
-        uint32_t sub_start = 8u * F->hdr_bytes;
+        for (int g = 0; g < NG; g++) pq[g] = prm[(i0 + 16u * g) >> (12u - o)];
+        const uint32_t lb = dsc[64u * (HC + sfi) + l0];
+        uint32_t sub_start = 8u * hdr_bytes;
         for (uint32_t t = 0; t < sidx; t++) sub_start += rdl(sbits, (int)t);
         sub_start -= 8u * base;
-
-        // ---- 1. PCM (double-buffered: DMA'd during the previous frame) -> samples
-        STAMP(7);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        STAMP(8);
-        __syncthreads();
-        STAMP(0);
         const uint32_t nn = jit ? 0xFFFFFFFFu : (uint32_t)__builtin_amdgcn_readfirstlane((int)misc[20]);
-        // the job record of the frame after next before the DMA: waiting for it then never
-        // waits for the DMA (vmcnt completes in order)
+        // the job record of the frame after next before the DMAs: waiting for it then never
+        // waits for them (vmcnt completes in order)
         FrameJob jnn{};
         if (nn < n_items) jnn = a.jobs[nn >> ssh];
+        // the next frame's descriptor into the other slot (landed by the next frame's top wait;
+        // this frame reads its own slot through `dsc`)
+        dsc_ready = !jit && nxt < n_items;
+        if (dsc_ready) {
+            dsc_dma(jn.slot, nxt & ssh, dslot ^ 1u);
+            dslot ^= 1u;
+        }
         if (dbuf && nxt < n_items)
             stage_dma_w(a.pcm, jn.pcm_off, (uint32_t *)(smem + (buf ? LY.buf0 : LY.buf1)), cw, cst, dcode, wave, NW, l, drh,
                         nxt & ssh);
@@ -298,8 +349,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             if constexpr (LPW > 0) {
                 int32_t c[LPW];
 #pragma unroll
-                for (int t = 0; t < LPW; t++) c[t] = __builtin_amdgcn_readfirstlane((int32_t)sd->coef[t < kLpcMax ? t : 0]);
-                const uint32_t shift = (uint32_t)(int32_t)sd->lpc_shift;
+                for (int t = 0; t < LPW; t++) c[t] = __builtin_amdgcn_readfirstlane((int32_t)(int16_t)coef[t < kLpcMax ? t : 0]);
+                const uint32_t shift = (uint32_t)lpc_shift;
                 // LPC runs on i32 samples only (contract step 0), so every product is a
                 // v_mad_i64_i32 even for 32-bit input; taps bucketed by order (c[t] = 0 past it)
                 auto lpc = [&](auto WT) {
@@ -331,7 +382,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             if (type == 0) len = 8u + bd;
             else if (type == 1) len = 8u + w;
             else len = 8u + w + k * bps + 6u + param_len + ((p0 & 0x80u) ? 5u : 0u) +
-                       (type == 3 ? 4u + 5u + k * sd->lpc_prec : 0u);
+                       (type == 3 ? 4u + 5u + k * lpc_prec : 0u);
         }
         if (type == 1) {
             len += SPL * bps;
@@ -359,7 +410,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         bar_lds();  // image zeroed
         STAMP(3);
         if (tid < 4 && half == 0) {
-            const uint32_t hv = F->hdr[tid];
+            const uint32_t hv = dsc[4u + tid];
             if (hv) atomicOr(&img[tid], hv);
         }
 
@@ -372,7 +423,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
                 bw.init(img, pos);
                 if (type == 0) {  // writeConstantSubframe: 0x00, value << waste in bd bits
                     bw.put(0, 8);
-                    bw.put(((uint64_t)sd->cval << w) & (~0ull >> (64 - bd)), bd);
+                    bw.put(((uint64_t)cval << w) & (~0ull >> (64 - bd)), bd);
                 } else {
                     // type code: VERBATIM 1, FIXED 8|k, LPC 0x20|(k-1) (build-defined)
                     const uint32_t tc = (type == 1) ? 1u : (type == 2 ? (8u | k) : (0x20u | (k - 1u)));
@@ -383,11 +434,11 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
                         for (int j = 0; j < KH; j++)  // warm-up samples
                             if ((uint32_t)j < k) bw.put((uint64_t)(int64_t)x[KH + j] & mask, bps);
                         if (type == 3) {
-                            const uint32_t prec = sd->lpc_prec;
+                            const uint32_t prec = lpc_prec;
                             bw.put(prec - 1u, 4);
-                            bw.put((uint32_t)(int32_t)sd->lpc_shift & 31u, 5);
+                            bw.put((uint32_t)lpc_shift & 31u, 5);
                             for (uint32_t t = 0; t < k; t++)
-                                bw.put((uint64_t)(int64_t)sd->coef[t] & (~0ull >> (64 - prec)), prec);
+                                bw.put((uint64_t)(int64_t)(int16_t)coef[t] & (~0ull >> (64 - prec)), prec);
                         }
                         bw.put((method << 4) | o, 6);
                         const uint32_t p0 = pq[0];
@@ -494,7 +545,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             // half and returns the other's: no fence (a release fence writes back the XCD's L2,
             // which the pack's output stores keep full -- measured 2.2x slower)
             unsigned long long *side =
-                (unsigned long long *)(a.desc + (uint64_t)job.slot * a.desc_stride + desc_side_off(F->n_out));
+                (unsigned long long *)(a.desc + (uint64_t)job.slot * a.desc_stride + desc_side_off(n_out_f));
             if (l == 0) {
                 const unsigned long long mine = (unsigned long long)(0x80000000u | (sb << 16) | (crc & 0xFFFFu)) << (32u * half);
                 const unsigned long long old = atomicOr(side, mine);
