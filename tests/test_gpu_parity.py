@@ -294,3 +294,58 @@ def test_multi_encode_matches_single(devices, n):
     ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, 2, 16, 44100, first_frame=200)
     assert sizes == ref_sizes
     assert got == ref, _diff_msg(got, ref)
+
+
+def _wide_order_frames(ch):
+    """32-bit frames at the edges of the u32 bestOrder certificate (fg_device.hpp step 5: the
+    differences in u32 when every order's range over the frame fits i32, else the i64 totals):
+    a sample range of exactly 2^31 - 1 (fast) and 2^31 (i64), INT_MIN present (order 0 null),
+    first differences of +-(2^31 - 1) (order 1 valid, order 2 null), smooth frames on either side of
+    the certificate (a ramp over exactly 2^31 - 1, sines of 0.49 and 0.999 full scale), and for
+    stereo a side channel outside i32 (L = INT_MAX, R = INT_MIN)."""
+    lo, hi = -(1 << 31), (1 << 31) - 1
+    rng = np.random.Generator(np.random.PCG64(55))
+    i = np.arange(4096)
+    frames = []
+    a = rng.integers(-(1 << 30), (1 << 30), size=4096)
+    a[100], a[200] = -(1 << 30), (1 << 30) - 1                     # range exactly 2^31 - 1
+    frames.append(a)
+    b = a.copy()
+    b[300] = 1 << 30                                                 # range 2^31
+    frames.append(b)
+    c = rng.integers(-1000, 1000, size=4096)
+    c[2000] = lo                                                     # INT_MIN: order 0 null
+    frames.append(c)
+    frames.append(np.where(i % 2 == 0, (1 << 30) - 1, -(1 << 30)))  # e1 = +-(2^31 - 1)
+    frames.append((np.sin(i / 700.0) * 0.999 * hi).astype(np.int64))  # large, smooth: i64 totals
+    frames.append((np.sin(i / 700.0) * 0.49 * hi).astype(np.int64))   # smooth, range < 2^31 - 1: u32
+    frames.append(np.round(np.linspace(-(1 << 30), (1 << 30) - 1, 4096)).astype(np.int64))  # range 2^31 - 1: u32
+    frames.append(rng.integers(lo, hi + 1, size=4096))              # full-scale noise
+    out = []
+    for f in frames:
+        f = np.clip(f.astype(np.int64), lo, hi)
+        if ch == 1:
+            out.append(f[:, None])
+        else:
+            r = np.clip(f // 2 + rng.integers(-5, 5, size=4096), lo, hi)
+            out.append(np.stack([f, r], axis=1))
+    if ch == 2:  # side outside i32 in some samples, inside in others
+        l_ = np.where(i % 3 == 0, hi, rng.integers(-1000, 1000, size=4096))
+        r_ = np.where(i % 3 == 0, lo, rng.integers(-1000, 1000, size=4096))
+        out.append(np.stack([l_, r_], axis=1))
+    return np.concatenate(out, axis=0)
+
+
+@pytest.mark.parametrize("ch,lpc", [(1, 0), (2, 0), (2, 12), (1, 12)])
+def test_32bit_fixed_order_certificate_edges(ch, lpc):
+    """bestOrder of 32-bit full frames (u32 fast path or the exact i64 totals) equals the oracle's
+    at every edge of the fast path's validity certificate."""
+    s = _wide_order_frames(ch)
+    pcm = synth.to_pcm_bytes(s, 32)
+    enc = gpu_encoder(ch, 32, 192000, **({"lpc_order": lpc} if lpc else {}))
+    ref, ref_sizes, _ = oracle_ref.encode_stream(pcm, ch, 32, 192000, **({"lpc": lpc} if lpc else {}))
+    got, sizes = enc.encode_frames(pcm)
+    assert sizes == ref_sizes, "per-frame sizes differ"
+    assert got == ref, _diff_msg(got, ref)
+    dec, _ = oracle_ref.decode_frames(got, ch, 32, 192000, len(s))
+    assert dec == pcm

@@ -7,7 +7,8 @@ import flacgpu, synth
 
 NAMES = ["DMA issue+job load", "sample load", "waste+eq", "bestOrder", "rice pass", "param search (rest)",
          "desc+rec+bar", "stereo+exact", "ticket atomic", "vmcnt(0) wait", "top barrier",
-         "fixed rice search", "LPC load+autocorr", "LPC Levinson-Durbin", "LPC residual pass"]
+         "fixed rice search", "LPC load+autocorr", "LPC Levinson-Durbin", "LPC residual pass",
+         "bestOrder before i64"]
 PNAMES = ["top barrier", "offsets+bar", "zero img+bars", "residuals", "pack codes+bar", "CRC+bars", "store+bar",
           "ticket+desc loads", "vmcnt(0) wait", "DMA issue+sample load", "lane_bits/bits loads+scan"]
 S, F = int(os.environ.get("STAMP_S", "1024")), int(os.environ.get("STAMP_F", "32"))

@@ -103,7 +103,10 @@ __device__ __forceinline__ T dppT(T v, int which);
 #define FG_ADD(a, b) ((a) + (b))
 #define FG_OR(a, b) ((a) | (b))
 #define FG_XOR(a, b) ((a) ^ (b))
-#define FG_MAX(a, b) ((a) > (b) ? (a) : (b))
+// (a function, not a ternary: `b` is a DPP read, and a ternary evaluating it twice had the compiler
+// redo the read under the compare's exec mask, where a source lane that is switched off reads 0 --
+// the row maximum survived only in the lane that held it, and wave_max32 read lanes 0/16/32/48)
+#define FG_MAX(a, b) max((a), (b))
 FG_ROW_REDUCE(row_sum32, uint32_t, FG_ADD, dpp)
 FG_ROW_REDUCE(row_sum64, uint64_t, FG_ADD, dpp64)
 FG_ROW_REDUCE(row_or32, uint32_t, FG_OR, dpp)
@@ -1455,8 +1458,19 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                 }
                 eq = (mx == (int32_t)x0) && (mn == (int32_t)x0);
             } else {
+                // the low words by max / min as above, the bit-32 mask against x0's sign
+                const uint32_t x0l = (uint32_t)x0;
+                uint32_t mx = x0l, mn = x0l;
 #pragma unroll
-                for (int j = 0; j < 64; j++) eq &= (wide_value(s[j], hb, j) == x0) || (!FULL && l * 64u + j >= n);
+                for (int j = 0; j < 64; j++) {
+                    const uint32_t v = (!FULL && l * 64u + j >= n) ? x0l : (uint32_t)s[j];
+                    mx = max(mx, v);
+                    mn = min(mn, v);
+                }
+                const uint32_t nv = FULL ? 64u : (n > l * 64u ? min(n - l * 64u, 64u) : 0u);
+                const uint64_t vm = nv >= 64u ? ~0ull : ((1ull << nv) - 1ull);
+                const uint64_t hx = x0 < 0 ? ~0ull : 0ull;
+                eq = mx == x0l && mn == x0l && ((hb ^ hx) & vm) == 0ull;
             }
             if (__all(eq)) {
                 R.type = 0;
@@ -1599,37 +1613,115 @@ __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LP
                     T[4] = wave_sum64(T4);
                 }
             } else {
-                // wide path (i64): an order is invalid if any |e| exceeds i32 (fixed.zig:160-162);
-                // applying the check for bps' < 28 too is a no-op there, so one path serves both
-                int64_t p0 = h1, p1 = h1 - h2, p2 = h1 - 2 * h2 + h3, p3 = h1 - 3 * h2 + 3 * h3 - h4;
-                uint64_t A0 = 0, A1 = 0, A2 = 0, A3 = 0, A4 = 0, O0 = 0, O1 = 0, O2 = 0, O3 = 0, O4 = 0;
+                // 32-bit input.  Full frames first try the differences in u32: the low words are
+                // exact mod 2^32 and the biased words b_q = e_q + 0x7FFFFFFF (b_{q+1} = (b_q[prev] ^
+                // 0x7FFFFFFF) + b_q, as in the narrow path) are the exact e_q + 0x7FFFFFFF while e_q
+                // lies in [-2^31 + 1, 2^31 - 1]; then |e_{q+1}| = v_sad_u32(b_q, b_q[prev]) is exact.
+                // Certificate, from each order's range of b over the wave's counted samples: if
+                // e_0 fits i32 (the side: bit 32 == bit 31) and is never -2^31, and max b_q - min b_q
+                // <= 2^31 - 1 for q = 0..3, every e_{q+1} lies in [-(2^31 - 1), 2^31 - 1] -- so all
+                // five orders are valid (fixed.zig:160-162) and every total exact.  Otherwise the
+                // totals are redone in i64 below.  c5 stamps: this phase was 15 % of an analysis
+                // wave's time on i64 arithmetic (r5q).
+                bool done = false;
+                if constexpr (FULL) {
+                    uint32_t nf = 0;  // the side's 33-bit samples: bit 32 != bit 31 somewhere
+                    if (stereo && cand == 3) {
 #pragma unroll
-                for (int j = 0; j < 64; j++) {
-                    const bool valid = FULL || (l * 64u + j < n);
-                    const bool z = (l == 0);
-                    const int64_t e0 = wide_value(s[j], hb, j), e1 = e0 - p0, e2 = e1 - p1, e3 = e2 - p2,
-                                  e4 = e3 - p3;
-                    const uint64_t a0 = (uint64_t)(e0 < 0 ? -e0 : e0), a1 = (uint64_t)(e1 < 0 ? -e1 : e1),
-                                   a2 = (uint64_t)(e2 < 0 ? -e2 : e2), a3 = (uint64_t)(e3 < 0 ? -e3 : e3),
-                                   a4 = (uint64_t)(e4 < 0 ? -e4 : e4);
-                    const bool v0 = valid, v1 = valid && !(z && j < 1), v2 = valid && !(z && j < 2),
-                               v3 = valid && !(z && j < 3), v4 = valid && !(z && j < 4);
-                    A0 += v0 ? a0 : 0; O0 |= v0 ? a0 : 0;
-                    A1 += v1 ? a1 : 0; O1 |= v1 ? a1 : 0;
-                    A2 += v2 ? a2 : 0; O2 |= v2 ? a2 : 0;
-                    A3 += v3 ? a3 : 0; O3 |= v3 ? a3 : 0;
-                    A4 += v4 ? a4 : 0; O4 |= v4 ? a4 : 0;
-                    p0 = e0; p1 = e1; p2 = e2; p3 = e3;
-                    // keep the ten accumulations serial: reassociated into trees they would hold all
-                    // 64 terms of each live at once (hundreds of VGPRs, spilled)
-                    asm volatile("" : "+v"(A0), "+v"(A1), "+v"(A2), "+v"(A3), "+v"(A4));
-                    asm volatile("" : "+v"(O0), "+v"(O1), "+v"(O2), "+v"(O3), "+v"(O4));
+                        for (int j = 0; j < 64; j++) nf |= ((uint32_t)(hb >> j) ^ ((uint32_t)s[j] >> 31)) & 1u;
+                    }
+                    if (__builtin_expect(!__any(nf != 0u), 1)) {  // (expect: the fast path laid out inline)
+                        const uint32_t KB = 0x7FFFFFFFu;
+                        const uint32_t u1 = (uint32_t)h1, u2 = (uint32_t)h2, u3 = (uint32_t)h3, u4 = (uint32_t)h4;
+                        uint32_t pb0 = u1 + KB;
+                        uint32_t pb1 = (u1 - u2) + KB;
+                        uint32_t pb2 = (u1 - 2u * u2 + u3) + KB;
+                        uint32_t pb3 = (u1 - 3u * u2 + 3u * u3 - u4) + KB;
+                        uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+                        uint32_t mx0 = 0, mx1 = 0, mx2 = 0, mx3 = 0, mn0 = ~0u, mn1 = ~0u, mn2 = ~0u, mn3 = ~0u;
+                        uint64_t A0 = 0, A1 = 0, A2 = 0, A3 = 0, A4 = 0;
+#pragma unroll
+                        for (int j = 0; j < 64; j++) {
+                            const uint32_t b0 = (uint32_t)s[j] + KB;
+                            const uint32_t b1 = (pb0 ^ KB) + b0;
+                            const uint32_t b2 = (pb1 ^ KB) + b1;
+                            const uint32_t b3 = (pb2 ^ KB) + b2;
+                            const uint32_t n0 = sad_u32(b0, KB, t0), n1 = sad_u32(b0, pb0, t1), n2 = sad_u32(b1, pb1, t2),
+                                           n3 = sad_u32(b2, pb2, t3), n4 = sad_u32(b3, pb3, t4);
+                            if (j < 4) {  // lane 0: e_q[i] for i < q neither counts (fixed.zig:102-127) nor bounds
+                                const bool z = (l == 0);
+                                t0 = n0;
+                                t1 = (z && j < 1) ? t1 : n1;
+                                t2 = (z && j < 2) ? t2 : n2;
+                                t3 = (z && j < 3) ? t3 : n3;
+                                t4 = z ? t4 : n4;
+                                mx0 = max(mx0, b0); mn0 = min(mn0, b0);
+                                mx1 = max(mx1, (z && j < 1) ? 0u : b1); mn1 = min(mn1, (z && j < 1) ? ~0u : b1);
+                                mx2 = max(mx2, (z && j < 2) ? 0u : b2); mn2 = min(mn2, (z && j < 2) ? ~0u : b2);
+                                mx3 = max(mx3, (z && j < 3) ? 0u : b3); mn3 = min(mn3, (z && j < 3) ? ~0u : b3);
+                            } else {
+                                t0 = n0; t1 = n1; t2 = n2; t3 = n3; t4 = n4;
+                                mx0 = max(mx0, b0); mn0 = min(mn0, b0);
+                                mx1 = max(mx1, b1); mn1 = min(mn1, b1);
+                                mx2 = max(mx2, b2); mn2 = min(mn2, b2);
+                                mx3 = max(mx3, b3); mn3 = min(mn3, b3);
+                            }
+                            if (j & 1) {  // two terms <= 2^31 - 1 fit u32 (certified below)
+                                A0 += t0; A1 += t1; A2 += t2; A3 += t3; A4 += t4;
+                                t0 = t1 = t2 = t3 = t4 = 0;
+                                // serial accumulations (reassociated trees hold every pair sum / bound live)
+                                asm volatile("" : "+v"(A0), "+v"(A1), "+v"(A2), "+v"(A3), "+v"(A4));
+                                asm volatile("" : "+v"(mx0), "+v"(mx1), "+v"(mx2), "+v"(mx3));
+                                asm volatile("" : "+v"(mn0), "+v"(mn1), "+v"(mn2), "+v"(mn3));
+                            }
+                            pb0 = b0; pb1 = b1; pb2 = b2; pb3 = b3;
+                            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // no hoisting of later samples' b0
+                        }
+                        const uint32_t M0 = wave_max32(mx0), M1 = wave_max32(mx1), M2 = wave_max32(mx2),
+                                       M3 = wave_max32(mx3);
+                        const uint32_t m0 = ~wave_max32(~mn0), m1 = ~wave_max32(~mn1), m2 = ~wave_max32(~mn2),
+                                       m3 = ~wave_max32(~mn3);
+                        if (__builtin_expect(M0 != ~0u && M0 - m0 <= KB && M1 - m1 <= KB && M2 - m2 <= KB && M3 - m3 <= KB, 1)) {
+                            T[0] = wave_sum64(A0); T[1] = wave_sum64(A1); T[2] = wave_sum64(A2);
+                            T[3] = wave_sum64(A3); T[4] = wave_sum64(A4);
+                            done = true;
+                        }
+                    }
                 }
-                T[0] = wave_or64(O0) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A0);
-                T[1] = wave_or64(O1) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A1);
-                T[2] = wave_or64(O2) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A2);
-                T[3] = wave_or64(O3) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A3);
-                T[4] = wave_or64(O4) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A4);
+                if (__builtin_expect(!done, 0)) {  // the exact totals
+                    STAMP(15);  // (stamps build: bestOrder's time before a fallback)
+                    // wide path (i64): an order is invalid if any |e| exceeds i32 (fixed.zig:160-162);
+                    // applying the check for bps' < 28 too is a no-op there, so one path serves both
+                    int64_t p0 = h1, p1 = h1 - h2, p2 = h1 - 2 * h2 + h3, p3 = h1 - 3 * h2 + 3 * h3 - h4;
+                    uint64_t A0 = 0, A1 = 0, A2 = 0, A3 = 0, A4 = 0, O0 = 0, O1 = 0, O2 = 0, O3 = 0, O4 = 0;
+#pragma unroll
+                    for (int j = 0; j < 64; j++) {
+                        const bool valid = FULL || (l * 64u + j < n);
+                        const bool z = (l == 0);
+                        const int64_t e0 = wide_value(s[j], hb, j), e1 = e0 - p0, e2 = e1 - p1, e3 = e2 - p2,
+                                      e4 = e3 - p3;
+                        const uint64_t a0 = (uint64_t)(e0 < 0 ? -e0 : e0), a1 = (uint64_t)(e1 < 0 ? -e1 : e1),
+                                       a2 = (uint64_t)(e2 < 0 ? -e2 : e2), a3 = (uint64_t)(e3 < 0 ? -e3 : e3),
+                                       a4 = (uint64_t)(e4 < 0 ? -e4 : e4);
+                        const bool v0 = valid, v1 = valid && !(z && j < 1), v2 = valid && !(z && j < 2),
+                                   v3 = valid && !(z && j < 3), v4 = valid && !(z && j < 4);
+                        A0 += v0 ? a0 : 0; O0 |= v0 ? a0 : 0;
+                        A1 += v1 ? a1 : 0; O1 |= v1 ? a1 : 0;
+                        A2 += v2 ? a2 : 0; O2 |= v2 ? a2 : 0;
+                        A3 += v3 ? a3 : 0; O3 |= v3 ? a3 : 0;
+                        A4 += v4 ? a4 : 0; O4 |= v4 ? a4 : 0;
+                        p0 = e0; p1 = e1; p2 = e2; p3 = e3;
+                        // keep the ten accumulations serial: reassociated into trees they would hold all
+                        // 64 terms of each live at once (hundreds of VGPRs, spilled)
+                        asm volatile("" : "+v"(A0), "+v"(A1), "+v"(A2), "+v"(A3), "+v"(A4));
+                        asm volatile("" : "+v"(O0), "+v"(O1), "+v"(O2), "+v"(O3), "+v"(O4));
+                    }
+                    T[0] = wave_or64(O0) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A0);
+                    T[1] = wave_or64(O1) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A1);
+                    T[2] = wave_or64(O2) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A2);
+                    T[3] = wave_or64(O3) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A3);
+                    T[4] = wave_or64(O4) > 0x7FFFFFFFull ? ~0ull : wave_sum64(A4);
+                }
             }
             k = 0;
 #pragma unroll
