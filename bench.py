@@ -107,6 +107,8 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-files", default="8,16,32,64", help="file counts of the end-to-end curve")
     p.add_argument("--e2e-minutes", type=float, default=10.0)
+    p.add_argument("--e2e-max-frames", type=int, default=6144,
+                   help="frames per context of the end-to-end encoders (three pipelined chunk sets)")
     p.add_argument("--e2e-numa", choices=["local", "off"], default="local",
                    help="local: every thread of the process on the GPU's NUMA node before the e2e buffers "
                         "are allocated (pinned pages and the MD5 pool's reads on the GPU's side of the fabric)")
@@ -563,8 +565,8 @@ def end_to_end(args):
             k += 7
         files.append(buf)
     L = flacgpu.load_library()
-    # 6144 frames: three chunk sets of 2048 frames (32 MiB of PCM) for the pipelined schedule
-    encs = [flacgpu.Encoder(ch, bits, rate, device=0, max_frames=6144) for _ in files]
+    # 6144 frames (default): three chunk sets of 2048 frames (32 MiB of PCM) for the pipelined schedule
+    encs = [flacgpu.Encoder(ch, bits, rate, device=0, max_frames=args.e2e_max_frames) for _ in files]
     cap = 200 + ((n + 4095) // 4096 + 1) * encs[0].frame_bound()
     outs = [pinned(cap) for _ in files]
     lens = [ctypes.c_size_t(0) for _ in files]
