@@ -252,9 +252,10 @@ __device__ __forceinline__ uint32_t crc_from_q(uint32_t qp) {
 // front padding of an init-0 CRC), times e = z^(16 + 32 * words after them) mod Q; parity in bit 16.
 __device__ __forceinline__ uint32_t crc_lane_q(const uint32_t *img, int32_t va, uint32_t n, uint32_t e) {
     uint32_t s = 0, px = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const int32_t r = va + (int32_t)i;
-        const uint32_t w = r >= 0 ? img[r] : 0u;
+    // the padding words before the image leave an init-0 chain at 0: start past them instead of
+    // testing every index (the test put each load under its own exec mask)
+    for (uint32_t i = va < 0 ? (uint32_t)(-va) : 0u; i < n; i++) {
+        const uint32_t w = img[va + (int32_t)i];
         s = q_word(s, w);
         px ^= w;
     }
