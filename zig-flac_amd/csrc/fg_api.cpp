@@ -664,7 +664,7 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     const bool lpc = c->cfg.prediction != 0;
     // 24-bit LPC analysis runs three waves per SIMD (fg_device.hpp): double-buffer only where
     // three workgroups still fit the LDS
-    const uint32_t ana_wgs = (lpc && c->B == 3) ? 3u : 1u;
+    const uint32_t ana_wgs = (lpc && c->B == 3) ? (FG_C3_W == 3 ? 3u : 2u) : 1u;
     c->stage_dbuf = ana_layout(c->C, c->B, nw, true, true, lpc).total * ana_wgs <= 160u * 1024u;
     c->lds = ana_layout(c->C, c->B, nw, true, c->stage_dbuf, lpc).total;
     c->lds_tail = ana_layout(c->C, c->B, nw, false, false, lpc).total;

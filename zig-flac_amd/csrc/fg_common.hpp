@@ -11,6 +11,9 @@
 #ifndef FG_DIAG
 #define FG_DIAG 0
 #endif
+#ifndef FG_C3_W
+#define FG_C3_W 3  // waves per SIMD of the 24-bit LPC full-frame analysis (k_analyze; fg_api.cpp sizes its staging to match)
+#endif
 
 namespace fg {
 

@@ -1242,7 +1242,7 @@ template <int B, int CLS, bool FULL, int MAXT, int NC, int LPW, bool FP = false>
 // so three workgroups fit the LDS) beat two with double buffering: c3 analysis 5.56 -> 4.80 ms
 // (the 32-bit variant spills too much at 168: c5 8.7 -> 10.7 ms, so it stays at two).
 __global__ void __launch_bounds__(MAXT, ((MAXT == 256 && CLS != 32 && FULL && LPW == 0) ? FG_MINW
-                                          : ((FULL && LPW > 0 && CLS == 24) ? 3 : 2)))
+                                          : ((FULL && LPW > 0 && CLS == 24) ? FG_C3_W : 2)))
     k_analyze(EncodeArgs a) {
     if (a.enc_prio) __builtin_amdgcn_s_setprio(1);
     using ST = typename Cls<CLS>::S;
