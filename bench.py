@@ -75,11 +75,11 @@ sys.path.insert(0, os.path.join(ROOT, "zig-flac_amd"))
 
 METRIC = "MSamples/s encoded (whole node), 44.1kHz/16-bit stereo, blocksize 4096"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: measured float4 copy; BASELINE.md asks for the fraction of both
 # BASELINE.json configs (channels, bits, rate, LPC max order); c2 is the headline metric's
 PRESETS = {"c2": (2, 16, 44100, 0), "c3": (2, 24, 96000, 8), "c4": (8, 24, 96000, 0), "c5": (2, 32, 192000, 12)}
-# CPU-baseline sample per config (blocks, P threads; the one-core run takes 1/8 of it): about
-# 1-4 s of wall per run on the box's 16 cores at the measured per-core rates
-CPU_FRAMES = {"c2": 98304, "c3": 49152, "c4": 16384, "c5": 32768}
+# CPU-baseline input per config (blocks, 512 MiB-1.5 GiB of PCM; the fixed-time runs cycle over it)
+CPU_FRAMES = {"c2": 32768, "c3": 16384, "c4": 4096, "c5": 8192}
 LIMITER = {  # what binds each kernel (measured, not the roofline it is priced on)
     "analyze": "VALU issue/latency (integer dependent chains per lane), not HBM",
     "pack": "LDS atomics + dependent bit-offset chains, not HBM",
@@ -107,6 +107,8 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-files", default="8,16,32,64", help="file counts of the end-to-end curve")
     p.add_argument("--e2e-minutes", type=float, default=10.0)
+    p.add_argument("--e2e-node-files", type=int, default=32,
+                   help="files per rank of the every-rank end-to-end run (N > 1)")
     p.add_argument("--e2e-max-frames", type=int, default=6144,
                    help="frames per context of the end-to-end encoders (three pipelined chunk sets)")
     p.add_argument("--e2e-numa", choices=["local", "off"], default="local",
@@ -117,8 +119,15 @@ def parse():
     p.add_argument("--sharded-frames", type=int, default=8192, help="frames per rank per window (sharded mode)")
     p.add_argument("--sharded-steps", type=int, default=10)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--cpu-frames", type=int, default=98304, help="blocks in the CPU-baseline sample")
+    p.add_argument("--cpu-frames", type=int, default=32768, help="blocks of the CPU-baseline input (cycled)")
+    p.add_argument("--cpu-seconds", type=float, default=1.0,
+                   help="seconds per P-thread CPU-baseline run (the single-core run takes 1.5x)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0: the CPU share (OMP_NUM_THREADS), capped at a socket")
+    p.add_argument("--cpu-reps", type=int, default=3, help="CPU-baseline runs per leg (best, median and spread reported)")
+    p.add_argument("--cpu-place", choices=["idle", "socket0", "none"], default="idle",
+                   help="CPU-baseline thread placement: least busy physical cores / first socket-0 CPUs / unpinned")
+    p.add_argument("--cpu-only", action="store_true", help="run only the CPU-baseline legs (no torch, no GPU) and "
+                                                           "print them as one JSON line")
     p.add_argument("--configs", default="c3,c4,c5",
                    help="other BASELINE configs timed as their own lines after the headline ('' = none)")
     p.add_argument("--cfg-frames", type=int, default=65536, help="blocks per GPU per step of each --configs line")
@@ -380,8 +389,11 @@ def sharded_stream(args, rank, world, dist_mod, dev):
     enc = flacgpu.Encoder(ch, bits, rate, device=torch.cuda.current_device(), max_frames=F, lpc_order=lpc)
     d_pcm = torch.from_numpy(shard).to(dev)
     cstream = torch.cuda.Stream(dev)
+    # the gather through the C ABI: libflacgpu.so's own RCCL communicator (flacgpu_gather_frames_device),
+    # its id handed out over the torch process group
+    comm = flacgpu.Comm.from_process_group(dist_mod, None, torch.cuda.current_device())
     with torch.cuda.stream(cstream):
-        ss = parallel.ShardedStream(enc, F, dist=dist_mod, device=dev)
+        ss = parallel.ShardedStream(enc, F, dist=dist_mod, device=dev, comm=comm)
         for _ in range(2):
             ss.step(d_pcm.data_ptr())
         torch.cuda.synchronize()
@@ -439,7 +451,8 @@ def sharded_stream(args, rank, world, dist_mod, dev):
                "value": round(samples / dt / 1e6, 2), "unit": "MSamples/s",
                "ms_per_window": round(dt / args.sharded_steps * 1e3, 4),
                "kernel_ms_per_window": per,
-               "gather": "all_gather of (frames, bytes) counts, then batched point-to-point RCCL transfers into "
+               "gather": "flacgpu_gather_frames_device (C ABI, libflacgpu.so's own RCCL communicator): "
+                         "all_gather of (frames, bytes) counts, then grouped point-to-point RCCL transfers into "
                          "slices of one receive buffer (rank 0 encodes into its head in place)",
                "md5_amdahl": {"ms_per_window_one_host_core": round(md5_s * 1e3, 2),
                               "stream_cap_msamples_per_s": round(world * F * 4096 / md5_s / 1e6, 1),
@@ -449,6 +462,7 @@ def sharded_stream(args, rank, world, dist_mod, dev):
                "verified": f"rank 0's first {k} frames of the last window (frame numbers from {last_first}) vs "
                            "the restatement; device STREAMINFO replay of the window vs the host replay"}
     ss.close()
+    comm.close()
     enc.close()
     del d_pcm
     if own_group:
@@ -498,13 +512,13 @@ def _timed(fn):
     return time.perf_counter() - t0
 
 
-def gpu_local_cpus():
-    """CPUs of the GPU's NUMA node (sysfs local_cpulist of cuda:0's PCI device) that this process may
-    use, or None."""
+def gpu_local_cpus(device=0):
+    """CPUs of the GPU's NUMA node (sysfs local_cpulist of the device's PCI function) that this process
+    may use, or None."""
     import torch
 
     try:
-        pr = torch.cuda.get_device_properties(0)
+        pr = torch.cuda.get_device_properties(device)
         bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
         txt = open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip()
         cpus = set()
@@ -526,6 +540,92 @@ def move_process(cpus):
             pass
 
 
+def e2e_files(n_files, n, fb, ch, bits, rate, stream=11):
+    """n_files ten-minute-sized PCM buffers in pinned host memory, cut from one seeded pool."""
+    import numpy as np
+    import torch
+
+    import synth
+
+    pool_n = 4096 * 1024
+    pool = np.frombuffer(synth.to_pcm_bytes(synth.synth_samples(pool_n, ch, bits, rate, stream=stream), bits),
+                         dtype=np.uint8)
+    files = []
+    for i in range(n_files):
+        buf = torch.empty(n * fb, dtype=torch.uint8, pin_memory=True).numpy()
+        pos, k = 0, i
+        while pos < n:
+            take = min(n - pos, pool_n - 4096 * (k % 64))
+            a = 4096 * (k % 64) * fb
+            buf[pos * fb:(pos + take) * fb] = pool[a:a + take * fb]
+            pos += take
+            k += 7
+        files.append(buf)
+    return files
+
+
+def end_to_end_node(args, rank, world, dist, dev):
+    """The end-to-end contract on EVERY rank at once (N > 1): each rank encodes its own files
+    (host PCM -> .flac in host memory, one flacgpu_encode_files call on its GPU, MD5s on its share of
+    the host pool), the calls bracketed by barriers; node value = every rank's samples / the slowest
+    rank's wall.  File 0 of every rank is compared with the restatement's whole-file encode."""
+    import torch
+
+    import flacgpu
+
+    ch, bits, rate = 2, 16, 44100
+    n = int(args.e2e_minutes * 60 * rate)
+    fb = ch * 2
+    nf = args.e2e_node_files
+    local = gpu_local_cpus(torch.cuda.current_device()) if args.e2e_numa == "local" else None
+    saved_aff = os.sched_getaffinity(0)
+    if local:
+        move_process(local)
+    files = e2e_files(nf, n, fb, ch, bits, rate, stream=11 + rank)
+    L = flacgpu.load_library()
+    enc = flacgpu.Encoder(ch, bits, rate, device=torch.cuda.current_device(), max_frames=args.e2e_max_frames)
+    cap = 200 + ((n + 4095) // 4096 + 1) * enc.frame_bound()
+    outs = [torch.empty(cap, dtype=torch.uint8, pin_memory=True).numpy() for _ in files]
+    fp = (ctypes.c_void_p * nf)(*[f.ctypes.data for f in files])
+    op = (ctypes.c_void_p * nf)(*[o.ctypes.data for o in outs])
+    ns = (ctypes.c_uint64 * nf)(*([n] * nf))
+    caps = (ctypes.c_size_t * nf)(*([cap] * nf))
+    bl = (ctypes.c_size_t * nf)()
+
+    def call():
+        return L.flacgpu_encode_files(enc.ctx, nf, fp, 2, ns, op, caps, bl)
+
+    rc = call()  # warm-up (pool threads, pinned mappings)
+    walls = []
+    for _ in range(2):
+        dist.barrier()
+        t0 = time.perf_counter()
+        rc |= call()
+        dt = time.perf_counter() - t0
+        dist.barrier()
+        walls.append(dt)
+    wall = min(walls)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref
+
+    ok = rc == 0 and outs[0][: bl[0]].tobytes() == oracle_ref.encode_file(files[0].tobytes(), ch, bits, rate)
+    t = torch.tensor([wall, float(nf * n), 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    tmax = t.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    enc.close()
+    if local:
+        move_process(saved_aff)
+    max_wall, samples, bad = float(tmax[0].item()), float(t[1].item()), float(t[2].item())
+    return {"value": round(samples / max_wall / 1e6, 1), "unit": "MSamples/s", "ranks": world,
+            "files": nf * world, "files_per_rank": nf, "mode": "batch", "minutes_per_file": args.e2e_minutes,
+            "wall_ms": round(max_wall * 1e3, 2), "rank0_wall_ms": round(wall * 1e3, 2),
+            "path": "every rank at once: pinned host PCM -> .flac in pinned host memory, one flacgpu_encode_files "
+                    "call per rank on its own GPU (MD5s on that rank's share of the host pool); node value = "
+                    "sum of every rank's samples / the slowest rank's wall (barrier before and after)",
+            "output_ok": bad == 0}
+
+
 def end_to_end(args):
     """BASELINE.md end-to-end contract: host PCM buffers -> .flac files in host memory, as a curve
     over the number of files encoded at once, per file (one context + host thread each) and as one
@@ -542,31 +642,19 @@ def end_to_end(args):
     fb = ch * 2
     counts = sorted({int(x) for x in str(args.e2e_files).split(",") if x})
     saved_aff = os.sched_getaffinity(0)
-    local = gpu_local_cpus() if args.e2e_numa == "local" else None
+    local = gpu_local_cpus(torch.cuda.current_device()) if args.e2e_numa == "local" else None
     if local:
         move_process(local)  # before the buffers are allocated and first touched
     nmax = max(counts)
-    pool_n = 4096 * 1024
-    pool = np.frombuffer(synth.to_pcm_bytes(synth.synth_samples(pool_n, ch, bits, rate, stream=11), bits),
-                         dtype=np.uint8)
 
     def pinned(nbytes):
         return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
 
-    files = []
-    for i in range(nmax):
-        buf = pinned(n * fb)
-        pos, k = 0, i
-        while pos < n:
-            take = min(n - pos, pool_n - 4096 * (k % 64))
-            a = 4096 * (k % 64) * fb
-            buf[pos * fb:(pos + take) * fb] = pool[a:a + take * fb]
-            pos += take
-            k += 7
-        files.append(buf)
+    files = e2e_files(nmax, n, fb, ch, bits, rate)
     L = flacgpu.load_library()
     # 6144 frames (default): three chunk sets of 2048 frames (32 MiB of PCM) for the pipelined schedule
-    encs = [flacgpu.Encoder(ch, bits, rate, device=0, max_frames=args.e2e_max_frames) for _ in files]
+    encs = [flacgpu.Encoder(ch, bits, rate, device=torch.cuda.current_device(), max_frames=args.e2e_max_frames)
+            for _ in files]
     cap = 200 + ((n + 4095) // 4096 + 1) * encs[0].frame_bound()
     outs = [pinned(cap) for _ in files]
     lens = [ctypes.c_size_t(0) for _ in files]
@@ -638,7 +726,7 @@ def end_to_end(args):
     t0 = time.perf_counter()
     hashlib.md5(files[0]).digest()
     md5_s = time.perf_counter() - t0
-    d = torch.empty(len(files[0]), dtype=torch.uint8, device="cuda")
+    d = torch.empty(len(files[0]), dtype=torch.uint8, device=torch.cuda.current_device())
     src = torch.from_numpy(files[0])
     d.copy_(src, non_blocking=True)
     torch.cuda.synchronize()
@@ -702,96 +790,207 @@ def cpu_facts():
     return facts
 
 
-def socket0_cpus():
-    try:
-        txt = open("/sys/devices/system/node/node0/cpulist").read().strip()
-        cpus = []
-        for part in txt.split(","):
+def _cpulist(txt):
+    cpus = []
+    for part in txt.strip().split(","):
+        if part:
             a, _, b = part.partition("-")
             cpus += list(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def socket0_cpus():
+    try:
         avail = os.sched_getaffinity(0)
-        return [c for c in cpus if c in avail]
+        return [c for c in _cpulist(open("/sys/devices/system/node/node0/cpulist").read()) if c in avail]
     except Exception:
         return sorted(os.sched_getaffinity(0))
 
 
-def _cpu_run(L, oracle_ref, buf, args, P, frames, cpus, lpc):
-    """P pinned threads, each encoding whole 8-block streams (incl. MD5) of `buf`; -> (samples, s)."""
+def cpu_busy(interval=0.3):
+    """Busy fraction of every CPU of this process's mask over `interval` seconds (/proc/stat), or {}."""
+    def snap():
+        d = {}
+        for line in open("/proc/stat"):
+            if line.startswith("cpu") and line[3:4].isdigit():
+                f = line.split()
+                v = [int(x) for x in f[1:]]
+                idle = v[3] + (v[4] if len(v) > 4 else 0)
+                d[int(f[0][3:])] = (sum(v), idle)
+        return d
+    try:
+        s0 = snap()
+        time.sleep(interval)
+        s1 = snap()
+    except Exception:
+        return {}
+    avail = os.sched_getaffinity(0)
+    out = {}
+    for c, (t1, i1) in s1.items():
+        if c in avail and c in s0:
+            dt = t1 - s0[c][0]
+            out[c] = 1.0 - (i1 - s0[c][1]) / dt if dt > 0 else 0.0
+    return out
+
+
+def pick_cores(P, place="idle"):
+    """P CPUs for the CPU-baseline threads, one per physical core.
+    idle    -- the least busy physical cores of the process's mask (/proc/stat over 0.3 s; a core's
+               load = its busiest SMT sibling), so that the sample does not share cores with other
+               work on the machine (the GPU box is one slice of a shared host: the first cores of
+               socket 0 are the ones everybody else's pinned threads land on too);
+    socket0 -- the first P CPUs of NUMA node 0 (rounds 1-5);
+    none    -- no pinning (the threads float)."""
+    if place == "none":
+        return None, {}
+    if place == "socket0":
+        return socket0_cpus(), {}
+    avail = sorted(os.sched_getaffinity(0))
+    busy = cpu_busy()
+    seen, cores = set(), []
+    for c in avail:
+        if c in seen:
+            continue
+        try:
+            sib = [x for x in _cpulist(open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read())
+                   if x in avail]
+        except Exception:
+            sib = [c]
+        seen.update(sib)
+        cores.append((max(busy.get(x, 0.0) for x in sib), c))
+    cores.sort()
+    chosen = [c for _, c in cores[:P]]
+    load = [round(b, 3) for b, _ in cores[:P]]
+    return chosen, {"physical_cores_in_mask": len(cores), "chosen_busy_max": max(load) if load else None,
+                    "chosen_busy_mean": round(sum(load) / len(load), 3) if load else None}
+
+
+def _cpu_run(L, oracle_ref, buf, args, P, seconds, cpus, lpc):
+    """P threads (thread t pinned to cpus[t], or floating if cpus is None), each encoding whole
+    8-block streams (incl. MD5) of `buf` one after another until `seconds` have passed: a fixed-time
+    throughput sample (no tail of one late thread); -> (samples, s) where s = the time the last
+    thread finished its last stream."""
     ch, bits = args.channels, args.bits
     fb = ch * (bits // 8)
     per_stream = 8 * 4096  # 8-block streams, the headline's shape
     n_streams_buf = len(buf) // (per_stream * fb)
-    per_thread = max(1, frames // P // 8)
     cfg = oracle_ref.config(ch, bits, args.rate, lpc=lpc)
     res = [0] * P
+    fin = [0.0] * P
     cap = 8 * L.oracle_max_frame_bytes(4096, bits, ch) + 64
+    go = threading.Barrier(P)
+    beg = [0.0] * P
 
     def run(t):
-        try:
-            os.sched_setaffinity(0, {cpus[t % len(cpus)]})  # this thread only
-        except Exception:
-            pass
+        if cpus:
+            try:
+                os.sched_setaffinity(0, {cpus[t % len(cpus)]})  # this thread only
+            except Exception:
+                pass
         out = ctypes.create_string_buffer(cap)
         sizes = (ctypes.c_uint32 * 8)()
         md5 = ctypes.create_string_buffer(16)
-        done = 0
-        for j in range(per_thread):
+        done, j = 0, 0
+        go.wait()  # threads placed and buffers allocated: the clock starts with the first encode
+        beg[t] = t0 = time.perf_counter()
+        while True:
             s = (t + j * P) % n_streams_buf
             base = buf.ctypes.data + s * per_stream * fb
             r = L.oracle_encode_stream(ctypes.byref(cfg), ctypes.c_void_p(base), bits // 8, ctypes.c_uint64(per_stream),
                                        ctypes.c_uint64(0), out, ctypes.c_size_t(cap), sizes, md5)
             done += per_stream if r > 0 else 0
-        res[t] = done
+            j += 1
+            now = time.perf_counter()
+            if now - t0 >= seconds:
+                break
+        res[t], fin[t] = done, now
 
     th = [threading.Thread(target=run, args=(t,)) for t in range(P)]
-    t0 = time.perf_counter()
     for t in th:
         t.start()
     for t in th:
         t.join()
-    return sum(res), time.perf_counter() - t0
+    return sum(res), max(fin) - min(beg)
 
 
-def cpu_baseline(buf, args):
+def _best_of(fn, reps):
+    """reps runs of fn() -> (samples, s); -> (best rate, [every rate]) in MSamples/s."""
+    rates = []
+    for _ in range(reps):
+        tot, dt = fn()
+        rates.append(tot / dt / 1e6)
+    return max(rates), rates
+
+
+def _spread(rates):
+    rs = sorted(rates)
+    return {"best": round(rs[-1], 3), "median": round(rs[len(rs) // 2], 3), "worst": round(rs[0], 3),
+            "spread": round((rs[-1] - rs[0]) / rs[-1], 4) if rs[-1] else None, "runs": [round(r, 3) for r in rates]}
+
+
+HEALTH_MIN = 0.9  # per-core rate at P threads / single-core rate below this: the sample was disturbed
+
+
+def cpu_baseline(buf, args, reps=None, place=None):
     """The CPU restatement (oracle/, built -O3 -march=x86-64-v4 as liboracle_fast.so): one thread
-    (one core, the reference's own shape: wav2flac is single-threaded) and P threads pinned to
-    distinct socket-0 cores, each encoding whole streams (incl. MD5).  LPC configs are also run
-    fixed-only, which is what the reference (no LPC, readme.md:27) does on the same input."""
+    (one core, the reference's own shape: wav2flac is single-threaded) and P threads on P distinct
+    physical cores, each encoding whole streams (incl. MD5); best of `reps` runs of each.  LPC
+    configs are also run fixed-only, which is what the reference (no LPC, readme.md:27) does on the
+    same input.  main() runs this BEFORE torch is imported or any HIP call is made (no GPU runtime
+    threads, no host MD5 pool, no pinned buffers yet), so the sample has the host to itself.
+    `health` = (P-thread rate / P) / single-core rate: below HEALTH_MIN the P-thread sample did not
+    scale (shared cores, clock drop) and the line says so."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref
 
+    reps = reps or args.cpu_reps
+    place = place or args.cpu_place
     L = oracle_ref.lib(fast=True)
     facts = cpu_facts()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
     P = args.cpu_threads or min(share, facts["cores_per_socket"] or share)
-    cpus = socket0_cpus()
     try:
         main_aff = os.sched_getaffinity(0)
     except Exception:
         main_aff = None
-    tot1, dt1 = _cpu_run(L, oracle_ref, buf, args, 1, max(8, args.cpu_frames // 8), cpus, args.lpc)
-    tot, dt = _cpu_run(L, oracle_ref, buf, args, P, args.cpu_frames, cpus, args.lpc)
+    cpus, pinfo = pick_cores(P, place)
+    if cpus is not None and len(cpus) < P:
+        P = len(cpus)  # fewer physical cores in the mask than the share: one thread per core
+    one_cpu = cpus[:1] if cpus else None
+    sec = args.cpu_seconds
+    best1, r1 = _best_of(lambda: _cpu_run(L, oracle_ref, buf, args, 1, 1.5 * sec, one_cpu, args.lpc), reps)
+    bestP, rP = _best_of(lambda: _cpu_run(L, oracle_ref, buf, args, P, sec, cpus, args.lpc), reps)
     fixed_only = None
     if args.lpc:
-        totf, dtf = _cpu_run(L, oracle_ref, buf, args, P, args.cpu_frames, cpus, 0)
-        fixed_only = {"value": round(totf / dtf / 1e6, 3), "cores": P,
+        bestf, rf = _best_of(lambda: _cpu_run(L, oracle_ref, buf, args, P, sec, cpus, 0), reps)
+        fixed_only = {"value": round(bestf, 3), "cores": P, **{k: v for k, v in _spread(rf).items() if k != "best"},
                       "note": "LPC off: the reference's own encoding of this input (it has no LPC)"}
     if main_aff:
         try:
             os.sched_setaffinity(0, main_aff)
         except Exception:
             pass
-    value = tot / dt / 1e6
     cps = facts["cores_per_socket"]
+    health = bestP / P / best1 if best1 else None
     return {
-        "value": round(value, 3),
+        "value": round(bestP, 3),
         "unit": "MSamples/s",
         "cores": P,
         "kind": "port",
-        "sample": f"{tot} samples ({tot // 4096} blocks as 8-block streams, incl. MD5), "
-                  f"{P} threads pinned to socket-0 cores, {dt:.2f}s wall ({dt * P:.1f} CPU-s)",
-        "single_core": {"value": round(tot1 / dt1 / 1e6, 3), "cores": 1,
-                        "sample": f"{tot1} samples ({tot1 // 4096} blocks), one thread on one core, {dt1:.2f}s"},
+        "sample": f"{P} threads on {P} physical cores ({place}) encoding 8-block streams (incl. MD5) of a "
+                  f"{len(buf) >> 20}-MiB input for {sec:g} s per run, best of {reps}, before any GPU/torch init",
+        "reps": reps,
+        "spread": _spread(rP),
+        "single_core": {"value": round(best1, 3), "cores": 1, **{k: v for k, v in _spread(r1).items() if k != "best"},
+                        "sample": f"one thread on one core for {1.5 * sec:g} s per run"},
+        "health": round(health, 4) if health else None,
+        "health_ok": bool(health and health >= HEALTH_MIN),
+        "health_note": (f"per-core rate at {P} threads / single-core rate (best samples); >= {HEALTH_MIN}: the "
+                        "P-thread sample scaled" if health and health >= HEALTH_MIN else
+                        f"per-core rate at {P} threads is {health:.2f} of single-core (< {HEALTH_MIN}): the "
+                        "P-thread sample did NOT scale linearly on this host (shared cores or all-core clock drop); "
+                        "the socket estimate below uses the measured per-core rate at P threads") if health else None,
+        "placement": {"mode": place, "cpus": cpus, **pinfo},
         "fixed_only": fixed_only,
         "lpc": args.lpc,
         "cpu_model": facts["model"],
@@ -800,12 +999,35 @@ def cpu_baseline(buf, args):
         "build": "oracle/flac_oracle.c -O3 -march=x86-64-v4 (C restatement, CRC-16 by slicing-by-8 tables "
                  "since r3w where the reference folds with PCLMUL; the Zig reference is unbuildable here: no "
                  "Zig 0.16 on the box)",
-        "per_core": round(value / P, 3),
-        "single_socket_estimate": round(value / P * cps, 1) if cps else None,
+        "per_core": round(bestP / P, 3),
+        "single_socket_estimate": round(bestP / P * cps, 1) if cps else None,
         "single_socket_note": f"measured at P = {P} threads (the box's CPU share for one GPU) of {cps} cores per "
-                              "socket; the socket figure scales the measured per-core rate linearly (an ESTIMATE, "
-                              "an upper bound: memory bandwidth and clocks are shared)",
+                              "socket; the socket figure scales the best P-thread sample's per-core rate linearly "
+                              "(an ESTIMATE, an upper bound: memory bandwidth and clocks are shared)",
     }
+
+
+def cpu_input(args, cfg, rank=0):
+    """The CPU legs' input: the same generator as the GPU step (build_input) for `cfg`, sized to the
+    CPU sample (CPU_FRAMES blocks), not to the GPU step."""
+    sub = argparse.Namespace(**vars(args))
+    sub.config = cfg
+    sub.channels, sub.bits, sub.rate, sub.lpc = PRESETS[cfg]
+    sub.cpu_frames = args.cpu_frames if cfg == (args.config or "c2") else CPU_FRAMES[cfg]
+    F = 16 if cfg == "c2" else 4  # blocks per stream of the GPU step (headline / --configs lines)
+    sub.frames = -(-sub.cpu_frames // F) * F
+    sub.streams = sub.frames // F
+    return sub, build_input(sub, rank)
+
+
+def cpu_legs(args, cfgs):
+    """Every CPU-baseline leg of the run, measured first (main() calls this before torch)."""
+    out = {}
+    for cfg in cfgs:
+        sub, buf = cpu_input(args, cfg)
+        out[cfg] = cpu_baseline(buf, sub)
+        del buf
+    return out
 
 
 # ---------------------------------------------------------------------------------------------
@@ -844,7 +1066,8 @@ def roofline_of(args, kt, steps, pcm_bytes, out_bytes, ms_per_step, key):
                      "weighted_issue_frac": round(counters["SQ_INSTS_VALU"] * cpi / avg / SIMD_CYCLES_PER_S, 4)
                      if cpi else None, "cycles_per_instr": cpi, "mix_source": msrc,
                      "waves_per_launch": counters.get("SQ_WAVES"), "source": src}
-        return {"achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(avg * 1e3, 4),
+        return {"achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5),
+                "frac_vs_6p29": round(ach / HBM_COPY_GBS, 5), "avg_launch_ms": round(avg * 1e3, 4),
                 "algorithmic_bytes_per_launch": algo[k], "traffic": traffic, "traffic_source": src,
                 "traffic_ratio": round(traffic / algo[k], 3) if traffic else None, "issue": issue}
 
@@ -887,6 +1110,7 @@ def roofline_of(args, kt, steps, pcm_bytes, out_bytes, ms_per_step, key):
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "frac_vs_6p29": round(achieved / HBM_COPY_GBS, 5),
         "hbm_frac": round(achieved / HBM_PEAK_GBS, 5),
         "traffic": rk[dom]["traffic"],
         "traffic_source": rk[dom]["traffic_source"],
@@ -912,7 +1136,7 @@ def workload_text(args, F):
             (", MD5 off (diagnostic)" if args.no_md5 else ", MD5 on its own HIP stream beside the next step's encode"))
 
 
-def config_line(args, cfg, dist, rank, world, dev):
+def config_line(args, cfg, dist, rank, world, dev, cpu=None):
     """One BASELINE config (c3 / c4 / c5) as its own timed line inside the default run: its preset,
     65536-block steps, barrier + max over ranks, output compared with the oracle after timing, the
     CPU port timed on rank 0 at N = 1 (one core, P cores, and fixed-only for the LPC configs)."""
@@ -956,8 +1180,8 @@ def config_line(args, cfg, dist, rank, world, dev):
                 "compression_ratio": round(out_bytes / pcm_bytes, 4),
                 "roofline": roofline_of(sub, kt, args.cfg_steps, pcm_bytes, out_bytes, ms, workload_key(sub)),
                 "output_ok": ok, "verified": vinfo, "cpu_baseline": None}
-        if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(buf, sub)
+        if cpu:  # measured before torch (main(), cpu_legs)
+            line["cpu_baseline"] = cpu
             line["vs_cpu_single_socket_estimate"] = (round(line["value"] / line["cpu_baseline"]["single_socket_estimate"], 1)
                                                      if line["cpu_baseline"].get("single_socket_estimate") else None)
     return line
@@ -982,7 +1206,8 @@ def _compact_roofline(r):
                  "issue": (v.get("issue") or {}).get("valu_issue_frac"),
                  "w_issue": (v.get("issue") or {}).get("weighted_issue_frac")}
     out = {"bound": r.get("bound"), "kernel": r.get("kernel"), "achieved": r.get("achieved"), "peak": r.get("peak"),
-           "unit": r.get("unit"), "frac": r.get("frac"), "traffic": r.get("traffic"),
+           "unit": r.get("unit"), "frac": r.get("frac"), "frac_vs_6p29": r.get("frac_vs_6p29"),
+           "peak_measured_copy": HBM_COPY_GBS, "traffic": r.get("traffic"),
            "traffic_ratio": (r.get("kernels") or {}).get(_dom_name(r), {}).get("traffic_ratio"),
            "algorithmic_bytes_per_launch": r.get("algorithmic_bytes_per_launch"),
            "avg_launch_ms": r.get("avg_launch_ms"), "step_issue_frac": r.get("step_issue_frac"),
@@ -1000,9 +1225,12 @@ def _dom_name(r):
 def _compact_cpu(c):
     if not c:
         return None
+    sp = c.get("spread") or {}
     return {"value": c.get("value"), "unit": c.get("unit"), "cores": c.get("cores"), "kind": c.get("kind"),
             "sample": c.get("sample", "")[:120],
+            "reps": c.get("reps"), "median": sp.get("median"), "spread": sp.get("spread"),
             "single_core": (c.get("single_core") or {}).get("value"),
+            "health": c.get("health"), "health_ok": c.get("health_ok"),
             "single_socket_estimate": c.get("single_socket_estimate"),
             "fixed_only": (c.get("fixed_only") or {}).get("value"), "cpu_model": c.get("cpu_model")}
 
@@ -1031,11 +1259,13 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
         cb = c.get("cpu_baseline") or {}
         cs[c["config"]] = {"value": c.get("value"), "ms_per_step": c.get("ms_per_step"),
                            "kernel_ms": c.get("kernel_ms_per_step"), "frac": r.get("frac"),
+                           "frac_vs_6p29": r.get("frac_vs_6p29"),
                            "step_issue_frac": r.get("step_issue_frac"),
                            "weighted_issue_frac": r.get("weighted_issue_frac"),
                            "traffic_ratio": (r.get("kernels") or {}).get(_dom_name(r), {}).get("traffic_ratio"),
                            "output_ok": c.get("output_ok"), "cpu": cb.get("value"),
-                           "cpu_single_core": (cb.get("single_core") or {}).get("value")}
+                           "cpu_single_core": (cb.get("single_core") or {}).get("value"),
+                           "cpu_health": cb.get("health")}
     line["configs"] = cs or None
     sc = full.get("stream_curve")
     if sc:
@@ -1046,6 +1276,7 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
     if e:
         top = max(e.get("curve") or [{}], key=lambda c: c.get("files", 0))
         line["end_to_end"] = {"value": e.get("value"), "files": e.get("files"), "mode": e.get("mode"),
+                              "ranks": e.get("ranks", 1),
                               "batch_frac_of_md5_bound": {str(c["files"]): c["batch"]["frac_of_md5_bound"]
                                                           for c in e.get("curve") or []},
                               "batch_h2d_d2h_gbs": e.get("batch_gbs"),
@@ -1172,12 +1403,24 @@ def main():
     # affinity mask: on the GPU box that mask is the whole machine, the share is OMP_NUM_THREADS
     if "FLACGPU_MD5_THREADS" not in os.environ and os.environ.get("OMP_NUM_THREADS", "1") not in ("", "1"):
         os.environ["FLACGPU_MD5_THREADS"] = os.environ["OMP_NUM_THREADS"]
-    import numpy as np
-    import torch
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the CPU baseline first (N = 1, or --cpu-only): before torch is imported and before any HIP call,
+    # host MD5 pool or pinned buffer exists, so its sample has the host to itself
+    headline = args.config or "c2"
+    other_cfgs = [c for c in (args.configs or "").split(",") if c] if not args.config else []
+    cpu_pre = {}
+    if args.cpu_only or (world == 1 and not args.no_cpu):
+        t0 = time.perf_counter()
+        cpu_pre = cpu_legs(args, [headline] + other_cfgs)
+        print(f"bench.py: CPU legs {time.perf_counter() - t0:.1f}s", file=sys.stderr)
+        if args.cpu_only:
+            os.write(json_fd, (json.dumps({"cpu_only": True, "legs": cpu_pre}) + "\n").encode())
+            return
+    import numpy as np
+    import torch
+
     if world > 1 and args.gpus not in (1, world):
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running {world} ranks", file=sys.stderr)
     dist = None
@@ -1230,6 +1473,11 @@ def main():
                                                   and not args.no_md5) else None
 
     curve = e2e = cpu = md5_rates = None
+    if world > 1 and not args.no_e2e and headline == "c2":
+        del d_pcm
+        d_pcm = None
+        torch.cuda.empty_cache()
+        e2e = end_to_end_node(args, rank, world, dist, dev)
     if rank == 0 and world == 1:
         if not args.no_curve and not args.no_md5:
             curve = stream_curve(args, enc, d_pcm, buf, fb, dev)
@@ -1238,8 +1486,7 @@ def main():
             del d_pcm
             torch.cuda.empty_cache()
             e2e = end_to_end(args)
-        if not args.no_cpu:
-            cpu = cpu_baseline(buf, args)
+        cpu = cpu_pre.get(headline)
     d_pcm = None
     enc.close()
     torch.cuda.empty_cache()
@@ -1248,7 +1495,7 @@ def main():
     configs = None
     if args.configs and not args.config:
         del buf
-        configs = [config_line(args, c, dist, rank, world, dev) for c in args.configs.split(",") if c]
+        configs = [config_line(args, c, dist, rank, world, dev, cpu_pre.get(c)) for c in other_cfgs]
 
     if e2e and cpu:
         e2e["vs_cpu_measured_P_cores"] = round(e2e["value"] / cpu["value"], 2)

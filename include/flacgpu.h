@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define FLACGPU_ABI_VERSION 4
+#define FLACGPU_ABI_VERSION 5
 
 /* the HIP null (legacy default) stream as a hip_stream argument */
 #define FLACGPU_STREAM_LEGACY ((void *)1)
@@ -123,6 +123,63 @@ void flacgpu_close_multi(flacgpu_multi *m);
 int flacgpu_multi_encode_frames(flacgpu_multi *m, const void *pcm, uint32_t bytes_per_sample, uint64_t n_samples,
                                 uint64_t first_frame_number, uint8_t *out, size_t out_cap, size_t *out_len,
                                 uint32_t *frame_bytes);
+
+/* ---- Multi-rank encode: one process per GPU, RCCL over xGMI (SURVEY.md §8(b)
+ *      "flacgpu_open_multi ... shards frames and gathers via RCCL", §8(e); BASELINE
+ *      config 4) -----------------------------------------------------------------
+ * The sharded form of wav2flac's block loop (wav2flac.zig:66-97): frame f of a
+ * stream depends only on its samples and its number (encoder.zig:234-284), so the
+ * ranks encode disjoint frames, and the only exchange is the gather of the
+ * variable-length bitstreams and the per-frame sizes (the u24 writeFrame returns,
+ * replayed by updateFrameSize in frame order, metadata.zig:35-40) to rank 0.
+ * librccl.so.1 is loaded on first use (an RCCL already in the process, e.g. a
+ * framework's, is reused; else /opt/rocm/lib); without it these return
+ * FLACGPU_ERR_DEVICE.  Every call below is collective: every rank of the
+ * communicator makes it, in the same order. */
+typedef struct flacgpu_comm flacgpu_comm;
+#define FLACGPU_COMM_ID_BYTES 128
+/* Rank 0 creates the communicator id; the host hands it to every rank (a file,
+ * a socket, torch.distributed's store: any channel).  No GPU work. */
+int flacgpu_comm_unique_id(uint8_t id[FLACGPU_COMM_ID_BYTES]);
+/* Join the communicator as `rank` of `world` on HIP device `device` (one rank
+ * per GPU: RCCL rejects two ranks on one device). */
+int flacgpu_comm_init(const uint8_t id[FLACGPU_COMM_ID_BYTES], int world, int rank, int device,
+                      flacgpu_comm **out);
+void flacgpu_comm_destroy(flacgpu_comm *comm);
+int flacgpu_comm_rank(const flacgpu_comm *comm);
+int flacgpu_comm_size(const flacgpu_comm *comm);
+
+/* Gather every rank's device-resident frames to rank 0, in rank order, into ONE
+ * device buffer (xGMI point-to-point; nothing crosses PCIe).  Each rank gives its
+ * n_frames frames: d_frames (device) holding nbytes valid bytes -- or, if
+ * d_nbytes is non-NULL, the count in device memory (a u64, e.g. the d_total of
+ * flacgpu_encode_plan_device_ex, read without a separate host sync) -- and
+ * d_sizes (device u32 per frame).  Rank 0 passes d_recv (capacity recv_cap
+ * bytes) and d_recv_sizes (capacity recv_sizes_cap entries); rank 0's own frames
+ * are copied to their head unless d_frames == d_recv (encoded in place).  Every
+ * rank gets *total_bytes / *total_frames (NULL: not wanted) = the gathered
+ * totals.  Queued on hip_stream (NULL: the HIP null stream) and synchronised
+ * with it once (the counts are read on the host to size the transfers).  If
+ * rank 0's capacities are too small, EVERY rank returns
+ * FLACGPU_ERR_OUTPUT_TOO_SMALL and nothing is transferred. */
+int flacgpu_gather_frames_device(flacgpu_comm *comm, const uint8_t *d_frames, uint64_t nbytes, const uint64_t *d_nbytes,
+                                 const uint32_t *d_sizes, uint64_t n_frames, uint8_t *d_recv, uint64_t recv_cap,
+                                 uint32_t *d_recv_sizes, uint64_t recv_sizes_cap, uint64_t *total_bytes,
+                                 uint64_t *total_frames, void *hip_stream);
+
+/* flacgpu_encode_frames across the ranks of comm: every rank passes the SAME
+ * arguments (pcm = the whole stream in host memory, e.g. each rank's mmap of the
+ * WAV data chunk; n_samples; first_frame_number).  The frames are cut into
+ * windows of world x max_frames_per_call frames; rank r encodes the r-th slice of
+ * every window on its GPU, and each window's frames are gathered to rank 0's GPU
+ * over RCCL and appended to rank 0's out (frame order).  Rank 0 gets exactly the
+ * bytes and frame sizes flacgpu_encode_frames would write for the whole input;
+ * other ranks get *out_len = 0 (out / frame_bytes unused, may be NULL).  A failure
+ * on any rank is returned by every rank.  ctx must be open on comm's device with
+ * the same config on every rank. */
+int flacgpu_encode_frames_sharded(flacgpu_ctx *ctx, flacgpu_comm *comm, const void *pcm, uint32_t bytes_per_sample,
+                                  uint64_t n_samples, uint64_t first_frame_number, uint8_t *out, size_t out_cap,
+                                  size_t *out_len, uint32_t *frame_bytes);
 
 /* Encoder.writeFrame for one frame, exactly the reference call: the caller
  * provides planar i32 samples (the reference's Encoder.samples[ch][0..n],

@@ -27,7 +27,27 @@ class OracleFrames:
         return out, sizes
 
 
-def run_windows(a, enc, dist, device):
+def run_capi(a, enc, comm, pcm):
+    """flacgpu_encode_frames_sharded (C ABI): every rank passes the whole stream, each encodes its
+    slice of every window, the library gathers over its own RCCL communicator; rank 0 assembles."""
+    import ctypes
+    import hashlib
+
+    import flacgpu
+
+    frames, sizes = comm.encode_frames_sharded(enc, pcm)
+    if comm.rank != 0:
+        assert frames == b"" and sizes == []
+        return None
+    n = len(pcm) // (a.channels * (a.bits // 8))
+    si = flacgpu.StreamInfo.new(a.rate, a.channels, a.bits, n, 4096)
+    for v in sizes:
+        si.update_frame_size(v)
+    ctypes.memmove(si.md5, hashlib.md5(pcm).digest(), 16)
+    return flacgpu.header_bytes(si, False) + flacgpu.vorbis_comment_bytes(True) + frames
+
+
+def run_windows(a, enc, dist, device, comm=None):
     """parallel.ShardedStream over a stream of windows x world x F whole frames: each rank holds
     only its shard of each window; rank 0 assembles the file (the bench's C4 sharded mode)."""
     import ctypes
@@ -45,7 +65,7 @@ def run_windows(a, enc, dist, device):
     per = a.channels * (a.bits // 8)
     n = a.windows * world * F * B
     pcm = synth.synth_pcm(n, a.channels, a.bits, a.rate)
-    ss = parallel.ShardedStream(enc, F, dist=dist, device=device)
+    ss = parallel.ShardedStream(enc, F, dist=dist, device=device, comm=comm)
     body = []
     for w in range(a.windows):
         s0 = (w * world + rank) * F * B
@@ -77,8 +97,12 @@ def main():
     p.add_argument("--md5", default="host")
     p.add_argument("--backend", choices=["gloo", "nccl"], default="gloo")
     p.add_argument("--out", required=True)
-    p.add_argument("--mode", choices=["file", "windows"], default="file",
-                   help="file: parallel.encode_sharded; windows: parallel.ShardedStream over --windows windows")
+    p.add_argument("--mode", choices=["file", "windows", "capi"], default="file",
+                   help="file: parallel.encode_sharded; windows: parallel.ShardedStream over --windows windows; "
+                        "capi: flacgpu_encode_frames_sharded")
+    p.add_argument("--gather", choices=["capi", "torch"], default="capi",
+                   help="GPU encoder under nccl: the gather through the C ABI (flacgpu.Comm) or torch.distributed")
+    p.add_argument("--max-frames", type=int, default=256, help="GPU encoder: frames per context call")
     p.add_argument("--windows", type=int, default=3)
     p.add_argument("--frames-per-rank", type=int, default=2)
     a = p.parse_args()
@@ -102,13 +126,20 @@ def main():
         import flacgpu
 
         enc = flacgpu.Encoder(a.channels, a.bits, a.rate, device=torch.cuda.current_device() if a.backend == "nccl"
-                              else 0, max_frames=max(256, a.frames_per_rank))
+                              else 0, max_frames=max(a.max_frames, a.frames_per_rank))
     else:
         enc = OracleFrames(a.channels, a.bits, a.rate)
-    if a.mode == "windows":
-        out = run_windows(a, enc, dist, device)
+    comm = None
+    if a.encoder == "gpu" and a.backend == "nccl" and a.gather == "capi":
+        comm = flacgpu.Comm.from_process_group(dist, None, torch.cuda.current_device())
+    if a.mode == "capi":
+        out = run_capi(a, enc, comm, pcm)
+    elif a.mode == "windows":
+        out = run_windows(a, enc, dist, device, comm)
     else:
-        out = parallel.encode_sharded(enc, pcm, dist=dist, device=device, md5=a.md5)
+        out = parallel.encode_sharded(enc, pcm, dist=dist, device=device, md5=a.md5, comm=comm)
+    if comm is not None:
+        comm.close()
     if dist.get_rank() == 0:
         open(a.out, "wb").write(out)
     dist.barrier()

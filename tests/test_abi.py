@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert flacgpu.load_library().flacgpu_abi_version() == 4
+    assert flacgpu.load_library().flacgpu_abi_version() == 5
 
 
 def test_config_default_matches_reference():

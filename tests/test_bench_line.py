@@ -37,6 +37,49 @@ def test_compact_line_fits_and_has_contract_keys():
     assert line["sharded_stream"]["value"] == full["sharded_stream"]["value"]
 
 
+def test_compact_line_round6_keys():
+    """the CPU baseline carries its spread and scaling health, the roofline
+    its fraction of the measured 6.29 TB/s copy rate beside the 8 TB/s spec, and the end-to-end
+    block its rank count (every rank runs it under --gpus N)."""
+    full = _full()
+    full["roofline"]["frac_vs_6p29"] = 0.18
+    full["cpu_baseline"].update(reps=3, spread={"best": 300.0, "median": 290.0, "worst": 280.0, "spread": 0.0667},
+                                health=0.95, health_ok=True)
+    full["end_to_end"]["ranks"] = 8
+    line = bench.compact_line(full, "x")
+    assert len(json.dumps(line)) <= bench.LINE_MAX
+    r = line["roofline"]
+    assert r["frac_vs_6p29"] == 0.18 and r["peak_measured_copy"] == bench.HBM_COPY_GBS
+    c = line["cpu_baseline"]
+    for k in ("reps", "median", "spread", "health", "health_ok"):
+        assert k in c, k
+    assert c["health_ok"] is True and c["spread"] == 0.0667
+    assert line["end_to_end"]["ranks"] == 8
+    for v in line["configs"].values():
+        assert "frac_vs_6p29" in v and "cpu_health" in v
+
+
+def test_cpu_pick_cores_one_per_physical_core():
+    cpus, info = bench.pick_cores(2, "idle")
+    assert len(cpus) == len(set(cpus)) <= 2
+    assert set(cpus) <= os.sched_getaffinity(0)
+    assert bench.pick_cores(2, "none")[0] is None
+
+
+def test_cpu_baseline_fields(monkeypatch):
+    """A tiny fixed-time CPU leg: best-of-N with spread, health = per-core at P / single-core."""
+    import argparse
+
+    args = argparse.Namespace(config="c2", configs="", channels=2, bits=16, rate=44100, lpc=0, cpu_frames=256,
+                              cpu_seconds=0.05, cpu_reps=2, cpu_place="idle", cpu_threads=2)
+    sub, buf = bench.cpu_input(args, "c2")
+    c = bench.cpu_baseline(buf, sub)
+    assert c["reps"] == 2 and len(c["spread"]["runs"]) == 2 and c["value"] == c["spread"]["best"]
+    assert c["cores"] <= 2 and c["single_core"]["value"] > 0
+    assert abs(c["health"] - c["value"] / c["cores"] / c["single_core"]["value"]) < 1e-3
+    assert c["health_ok"] == (c["health"] >= bench.HEALTH_MIN)
+
+
 def test_compact_line_survives_the_driver_tail():
     """The line the driver sees is the last 8,392 characters of stdout: with rank 0's one line the
     whole line is inside it and parses."""

@@ -280,6 +280,30 @@ def test_cpp_encoder_api_matches_oracle_file(tmp_path, ch, bits, rate, n):
     assert out.read_bytes() == oracle_ref.encode_file(pcm, ch, bits, rate)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,ch,bits,n,maxf", [(1, 2, 16, 21 * 4096 + 99, 8), (1, 8, 24, 5 * 4096, 2),
+                                                  (2, 2, 16, 21 * 4096 + 99, 4), (8, 2, 16, 64 * 4096 + 1, 4)])
+def test_cpp_sharded_encode_matches_oracle_file(tmp_path, world, ch, bits, n, maxf):
+    """tests/cpp/sharded_encode_test.cpp: BASELINE config 4's path driven through the C ABI alone
+    (no Python, no torch in the ranks): fork one process per GPU, flacgpu_comm_unique_id /
+    flacgpu_comm_init / flacgpu_encode_frames_sharded, rank 0 assembles the file.  One rank per GPU:
+    world > visible GPUs is skipped (RCCL refuses two ranks on one device)."""
+    import os
+    import subprocess
+
+    if not _has_gpu() or __import__("torch").cuda.device_count() < world:
+        pytest.skip(f"{world} rank(s) need {world} GPU(s)")
+    subprocess.check_call(["make", "-s", "-C", CPP_DIR, "build/sharded_encode_test"])
+    pcm = synth.synth_pcm(n, ch, bits, 44100)
+    raw = tmp_path / "x.raw"
+    raw.write_bytes(pcm)
+    out = tmp_path / "o.flac"
+    r = subprocess.run([os.path.join(CPP_DIR, "build", "sharded_encode_test"), str(raw), str(ch), str(bits), "44100",
+                        str(world), str(maxf), str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out.read_bytes() == oracle_ref.encode_file(pcm, ch, bits, 44100)
+
+
 @pytest.mark.parametrize("threads", ["1", "3"])
 def test_host_md5_pool_matches_plain_chain(threads):
     """fg_md5_host.cpp's hashing pool (the file path's MD5 engine: up to eight callers' chains

@@ -8,7 +8,8 @@ import sys
 import numpy as np
 import pytest
 
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "zig-flac_amd"))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "zig-flac_amd"))
 import flacgpu  # noqa: E402
 
 
@@ -169,3 +170,42 @@ def test_md5_many_vector_and_scalar_paths(avx512):
     env = dict(os.environ, FLACGPU_MD5_THREADS="3", FLACGPU_MD5_AVX512=avx512)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
+def _pool_workers(env, cpus=None):
+    """host_workers of a fresh process (the pool is sized once per process), optionally pinned."""
+    import subprocess
+
+    code = ("import os, sys; sys.path.insert(0, %r)\n" % os.path.join(ROOT, "zig-flac_amd") +
+            (f"os.sched_setaffinity(0, {set(cpus)!r})\n" if cpus else "") +
+            "import flacgpu; print(flacgpu.md5_rates().host_workers)")
+    e = {k: v for k, v in os.environ.items() if k not in ("FLACGPU_MD5_THREADS", "LOCAL_WORLD_SIZE")}
+    e.update(env)
+    r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return int(r.stdout.strip().splitlines()[-1])
+
+
+def _quota_cpus():
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        return 0 if q == "max" else -(-int(q) // int(period))
+    except (OSError, ValueError):
+        return 0
+
+
+@pytest.mark.skipif(len(os.sched_getaffinity(0)) < 2, reason="needs two CPUs")
+def test_pool_share_respects_a_rank_bound_mask():
+    """a process already bound to its share of the CPUs (numactl, SLURM
+    --cpu-bind, a per-rank cgroup) keeps that whole share as its MD5 pool even when the launcher sets
+    LOCAL_WORLD_SIZE; only a process that sees every online CPU divides by LOCAL_WORLD_SIZE."""
+    mine = sorted(os.sched_getaffinity(0))[:2]
+    quota = _quota_cpus()
+    assert _pool_workers({"LOCAL_WORLD_SIZE": "8"}, cpus=mine) == (min(quota, 2) if 0 < quota < 2 else 2)
+    aff = len(os.sched_getaffinity(0))
+    online = os.cpu_count()
+    whole = quota <= 0 and aff >= online
+    base = quota if 0 < quota < aff else aff
+    expect = max(1, base // 8) if whole else base
+    assert _pool_workers({"LOCAL_WORLD_SIZE": "8"}) == min(expect, 64)
+    assert _pool_workers({}) == min(base, 64)

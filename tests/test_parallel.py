@@ -109,3 +109,33 @@ def test_sharded_stream_windows_rccl_one_rank(tmp_path, ch, bits):
     n = 3 * 5 * 4096
     pcm = synth.synth_pcm(n, ch, bits, 44100)
     assert out == oracle_ref.encode_file(pcm, ch, bits, 44100)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nproc,ch,bits,n,maxf", [(1, 2, 16, 40 * 4096 + 777, 16), (1, 8, 24, 9 * 4096 + 5, 4),
+                                                  (1, 2, 32, 3 * 4096, 1), (2, 2, 16, 40 * 4096 + 777, 16),
+                                                  (4, 2, 24, 11 * 4096 + 1, 2), (8, 2, 16, 70 * 4096 + 3, 4)])
+def test_encode_frames_sharded_c_abi(tmp_path, nproc, ch, bits, n, maxf):
+    """the sharded encode behind the C ABI (flacgpu_encode_frames_sharded): every
+    rank passes the whole stream, encodes its slice of each window of world x max_frames frames, and
+    libflacgpu.so gathers the windows over its own RCCL communicator into rank 0's output in frame
+    order; the assembled file equals the restatement's whole-file encode.  Windows smaller than the
+    stream (max_frames 1..16) make every rank run several gather rounds and the last window ragged.
+    More than one rank needs that many GPUs (RCCL refuses two ranks on one device)."""
+    if _gpus() < nproc:
+        pytest.skip(f"RCCL needs one GPU per rank: {nproc} ranks, {_gpus()} GPU(s)")
+    out = run_workers(tmp_path, nproc, "--encoder", "gpu", "--backend", "nccl", "--mode", "capi", "--channels",
+                      str(ch), "--bits", str(bits), "--samples", str(n), "--max-frames", str(maxf))
+    pcm = synth.synth_pcm(n, ch, bits, 44100)
+    assert out == oracle_ref.encode_file(pcm, ch, bits, 44100)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gather", ["capi", "torch"])
+def test_sharded_gpu_gather_paths_one_rank(tmp_path, gather):
+    """parallel.encode_sharded with the C-ABI gather (flacgpu.Comm) and with the torch.distributed
+    one: the same file."""
+    n = 12 * 4096 + 999
+    out = run_workers(tmp_path, 1, "--encoder", "gpu", "--backend", "nccl", "--gather", gather, "--samples", str(n))
+    pcm = synth.synth_pcm(n, 2, 16, 44100)
+    assert out == oracle_ref.encode_file(pcm, 2, 16, 44100)

@@ -17,6 +17,8 @@
 #                                                          AB_ARGS; rows -> gpurun_out/ab_<tag>.txt
 #   tools/gpu.sh stamps <tag>                              phase stamps (build_st: make OUT=build_st
 #                                                          EXTRA=-DFG_STAMPS) for C2 and the wide configs
+#   tools/gpu.sh cpuplace <tag>                            CPU-baseline legs alone (no GPU) under each thread
+#                                                          placement -> gpurun_out/<tag>_cpu_<place>.json
 #   tools/gpu.sh final  <tag>                              tests + smoke + profiles of every config at
 #                                                          its bench workload + the default bench line
 set -o pipefail
@@ -118,6 +120,18 @@ do_stamps() {
   done
 }
 
+do_cpuplace() {
+  for place in socket0 idle none; do
+    timeout -k 10 300 python -u bench.py --cpu-only --cpu-place $place --configs=c5 > gpurun_out/${TAG}_cpu_$place.json 2> gpurun_out/${TAG}_cpu_$place.err ||
+      { tail -5 gpurun_out/${TAG}_cpu_$place.err; return 1; }
+    python3 -c "
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+for k, v in d['legs'].items():
+    print(sys.argv[2], k, v['value'], v['single_core']['value'], v['health'], v['spread']['runs'], v['single_core']['runs'], v['placement'].get('chosen_busy_max'))" gpurun_out/${TAG}_cpu_$place.json $place
+  done
+}
+
 case $CMD in
   tests) do_tests "$@" ;;
   smoke) do_smoke ;;
@@ -125,6 +139,7 @@ case $CMD in
   profile) do_profile "$TAG" "$@" ;;
   ab) do_ab "$@" ;;
   stamps) do_stamps ;;
+  cpuplace) do_cpuplace ;;
   final)
     do_tests && do_smoke &&
     do_profile ${TAG}_c2 c2 262144 16384 > gpurun_out/${TAG}_prof_c2.log 2>&1 &&

@@ -572,6 +572,10 @@ int fg::ctx_download_chunk(flacgpu_ctx *c, uint8_t *out, uint64_t total) {
 }
 
 uint32_t fg::ctx_max_frames(const flacgpu_ctx *c) { return c->max_frames; }
+fg::CtxDevice fg::ctx_device(const flacgpu_ctx *c) {
+    return {c->device, (void *)c->stream, c->d_out, c->d_fbytes, c->d_total, c->out_cap, c->C, c->B,
+            c->cfg.block_size};
+}
 void fg::ctx_finish(flacgpu_ctx *c) { resolve_timing(c); }
 
 extern "C" {

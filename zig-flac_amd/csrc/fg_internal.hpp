@@ -20,5 +20,17 @@ int ctx_download_chunk(flacgpu_ctx *c, uint8_t *out, uint64_t total);
 int ctx_encode_segments(flacgpu_ctx *c, uint32_t n, const uint8_t *const *src, const uint64_t *n_samples,
                         uint8_t *const *out, const size_t *out_cap, size_t *out_len, uint32_t *const *frame_bytes);
 uint32_t ctx_max_frames(const flacgpu_ctx *c);
+// The device side of a context: where ctx_encode_chunk leaves its frames (d_out), their sizes
+// (d_fbytes) and their byte total (d_total), on `stream` of HIP device `device`.
+struct CtxDevice {
+    int device;
+    void *stream;  // hipStream_t
+    uint8_t *d_out;
+    uint32_t *d_fbytes;
+    uint64_t *d_total;
+    uint64_t out_cap;
+    uint32_t channels, bytes_per_sample, block_size;
+};
+CtxDevice ctx_device(const flacgpu_ctx *c);
 void ctx_finish(flacgpu_ctx *c);  // fold pending timing events
 }  // namespace fg

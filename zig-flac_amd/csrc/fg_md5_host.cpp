@@ -268,6 +268,25 @@ struct Md5Job {
     size_t *left = nullptr;  // a batch's count of unfinished jobs (run_many)
 };
 
+}  // namespace
+
+// The pool size from the CPU facts.  One process per GPU (torchrun sets LOCAL_WORLD_SIZE): the
+// node's ranks share the CPUs, so each rank's pool takes its 1/LOCAL_WORLD_SIZE -- but only when
+// this process sees the whole machine (affinity mask = every online CPU, no cgroup quota).  A mask
+// or quota narrower than that is already this rank's share (numactl, SLURM --cpu-bind, a per-rank
+// cgroup) and is used as it is.
+int md5_pool_share_of(int quota_cpus, int aff, int online, const char *local_world) {
+    int n = (quota_cpus > 0 && quota_cpus < aff) ? quota_cpus : aff;
+    const bool whole_machine = quota_cpus <= 0 && aff >= online;
+    if (local_world && whole_machine) {
+        const int lw = std::atoi(local_world);
+        if (lw > 1) n = std::max(1, n / lw);
+    }
+    return n;
+}
+
+namespace {
+
 class Md5Pool {
   public:
     static Md5Pool &get() {
@@ -380,26 +399,20 @@ class Md5Pool {
     // affinity mask), else the affinity mask.  Not OMP_NUM_THREADS: launchers such as torchrun
     // set it to 1 per process, which would put every file's chain on one worker.
     static int cpu_share() {
-        int n = 0;
+        int quota_cpus = 0;
         if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
             char q[32] = {};
             long long period = 0;
             if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
                 const long long quota = atoll(q);
-                if (quota > 0) n = (int)((quota + period - 1) / period);
+                if (quota > 0) quota_cpus = (int)((quota + period - 1) / period);
             }
             fclose(f);
         }
         cpu_set_t set;
         const int aff = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
-        n = (n > 0 && n < aff) ? n : aff;
-        // one process per GPU (torchrun sets LOCAL_WORLD_SIZE): the node's ranks share the CPUs,
-        // so each rank's pool takes its share, not the whole mask
-        if (const char *e = std::getenv("LOCAL_WORLD_SIZE")) {
-            const int lw = std::atoi(e);
-            if (lw > 1) n = std::max(1, n / lw);
-        }
-        return n;
+        const long online = sysconf(_SC_NPROCESSORS_ONLN);
+        return md5_pool_share_of(quota_cpus, aff, online > 0 ? (int)online : aff, std::getenv("LOCAL_WORLD_SIZE"));
     }
     Md5Pool() : owner_(getpid()) {
         int n = 0;

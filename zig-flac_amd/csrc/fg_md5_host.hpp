@@ -27,13 +27,18 @@ struct HostMd5 {
 // several times faster per core than one scalar chain each; more chains than fit the workers are
 // time-sliced.  Blocks until done.
 // FLACGPU_MD5_THREADS sets the worker count (default: the process's CPU share -- the cgroup quota,
-// else the affinity mask's CPUs, divided by LOCAL_WORLD_SIZE when a launcher sets it; -1: no
+// else the affinity mask's CPUs, divided by LOCAL_WORLD_SIZE when a launcher sets it and the
+// process sees the whole machine; -1: no
 // pool, each caller hashes its own chain).
 void md5_pool_update(HostMd5 *h, const void *data, size_t len);
 
 // hs[i]->update(data[i], lens[i]) for n independent chains on the pool, queued together (the
 // plan path's host engine: every stream segment of a batch at once).  Blocks until all are done.
 void md5_pool_update_many(HostMd5 *const *hs, const uint8_t *const *data, const size_t *lens, size_t n);
+
+// the pool's default size: the cgroup quota (quota_cpus > 0) or the affinity mask's CPUs, divided
+// by LOCAL_WORLD_SIZE only when the process sees every online CPU under no quota
+int md5_pool_share_of(int quota_cpus, int aff, int online, const char *local_world);
 
 // the pool's worker count (0: every caller hashes its own chain)
 int md5_pool_workers();

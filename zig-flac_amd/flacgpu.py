@@ -201,6 +201,72 @@ def wav_to_flac(wav: bytes, device: int = 0) -> bytes:
     return out.raw[: n.value]
 
 
+class Comm:
+    """flacgpu_comm: one rank of a multi-GPU communicator (RCCL over xGMI inside libflacgpu.so):
+    the bitstream gather of the sharded encode (wav2flac.zig:66-97 cut into
+    ranks, updateFrameSize replayed in frame order on rank 0, metadata.zig:35-40)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, comm_id: bytes, world: int, rank: int, device: int):
+        self.world, self.rank, self.device = world, rank, device
+        self.comm = ctypes.c_void_p()
+        cid = (ctypes.c_uint8 * self.ID_BYTES).from_buffer_copy(comm_id)
+        _check(load_library().flacgpu_comm_init(cid, world, rank, device, ctypes.byref(self.comm)), "comm_init")
+
+    @staticmethod
+    def unique_id() -> bytes:
+        cid = (ctypes.c_uint8 * Comm.ID_BYTES)()
+        _check(load_library().flacgpu_comm_unique_id(cid), "comm_unique_id")
+        return bytes(cid)
+
+    @classmethod
+    def from_process_group(cls, dist, group=None, device: int = 0) -> "Comm":
+        """Rank 0 of `group` makes the id, torch.distributed hands it to every rank (any backend)."""
+        rank = dist.get_rank(group)
+        box = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        return cls(box[0], dist.get_world_size(group), rank, device)
+
+    def gather_device(self, d_frames: int, nbytes: int, d_sizes: int, n_frames: int, d_recv: int = 0,
+                      recv_cap: int = 0, d_recv_sizes: int = 0, recv_sizes_cap: int = 0, d_nbytes: int = 0,
+                      stream=None):
+        """flacgpu_gather_frames_device -> (total bytes, total frames) gathered on rank 0."""
+        tb, tf = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(load_library().flacgpu_gather_frames_device(
+            self.comm, d_frames or None, nbytes, d_nbytes or None, d_sizes or None, n_frames, d_recv or None,
+            recv_cap, d_recv_sizes or None, recv_sizes_cap, ctypes.byref(tb), ctypes.byref(tf), stream),
+            "gather_frames_device")
+        return tb.value, tf.value
+
+    def encode_frames_sharded(self, enc, pcm: bytes, first_frame: int = 0):
+        """flacgpu_encode_frames_sharded: every rank passes the whole stream; rank 0 gets (frames,
+        sizes) exactly as flacgpu_encode_frames would write them, the others (b"", [])."""
+        B = enc.bits // 8
+        n = len(pcm) // (enc.channels * B)
+        nf = (n + enc.block_size - 1) // enc.block_size
+        cap = max(nf, 1) * enc.frame_bound() + 64 if self.rank == 0 else 0
+        out = ctypes.create_string_buffer(max(cap, 1))
+        fb = (ctypes.c_uint32 * max(nf, 1))()
+        n_out = ctypes.c_size_t(0)
+        _check(load_library().flacgpu_encode_frames_sharded(enc.ctx, self.comm, pcm, B, n, first_frame, out, cap,
+                                                            ctypes.byref(n_out), fb), "encode_frames_sharded")
+        if self.rank != 0:
+            return b"", []
+        return out.raw[: n_out.value], list(fb)[:nf]
+
+    def close(self):
+        if self.comm:
+            load_library().flacgpu_comm_destroy(self.comm)
+            self.comm = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 _lib = None
 
 
@@ -276,6 +342,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "flacgpu_open_multi": (I32, [I32, P, ctypes.POINTER(Config), U32, ctypes.POINTER(P)]),
         "flacgpu_close_multi": (None, [P]),
         "flacgpu_multi_encode_frames": (I32, [P, P, U32, U64, U64, P, SZ, ctypes.POINTER(SZ), P]),
+        "flacgpu_comm_unique_id": (I32, [P]),
+        "flacgpu_comm_init": (I32, [P, I32, I32, I32, ctypes.POINTER(P)]),
+        "flacgpu_comm_destroy": (None, [P]),
+        "flacgpu_comm_rank": (I32, [P]),
+        "flacgpu_comm_size": (I32, [P]),
+        "flacgpu_gather_frames_device": (I32, [P, P, U64, P, P, U64, P, U64, P, U64, ctypes.POINTER(U64),
+                                               ctypes.POINTER(U64), P]),
+        "flacgpu_encode_frames_sharded": (I32, [P, P, P, U32, U64, U64, P, SZ, ctypes.POINTER(SZ), P]),
     }
     # an older build named by FLACGPU_LIB (same-box A/B runs, tools/ab.sh) may predate later entry
     # points: those stay unbound there; the in-tree library must export every one
@@ -307,6 +381,8 @@ def exported_symbols() -> list:
         "flacgpu_get_config", "flacgpu_wav_parse", "flacgpu_streaminfo_init", "flacgpu_streaminfo_update_frame_size",
         "flacgpu_streaminfo_bytes", "flacgpu_header_bytes", "flacgpu_vorbis_comment_bytes", "flacgpu_encode_file", "flacgpu_encode_files",
         "flacgpu_wav_to_flac", "flacgpu_open_multi", "flacgpu_close_multi", "flacgpu_multi_encode_frames",
+        "flacgpu_comm_unique_id", "flacgpu_comm_init", "flacgpu_comm_destroy", "flacgpu_comm_rank",
+        "flacgpu_comm_size", "flacgpu_gather_frames_device", "flacgpu_encode_frames_sharded",
     ]
 
 

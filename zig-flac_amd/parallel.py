@@ -16,6 +16,11 @@ to the rank that writes the file:
   * rank 0 replays updateFrameSize in frame order (metadata.zig:35-40), copies the
     bitstream to the host once and writes the 73-byte header (encoder.zig:177-226).
 
+With a GPU encoder the gather runs inside libflacgpu.so (flacgpu.Comm: the C ABI's
+flacgpu_gather_frames_device over the library's own RCCL communicator, so a host in any
+language -- the reference's Zig -- drives the same path); torch.distributed moves the
+tensors only for the CPU encoder of the gloo tests.
+
 The stream MD5 is sequential over the whole stream and does not shard: rank 0
 computes it on a host thread that overlaps the encode and the gather (md5="host",
 the Amdahl term of SURVEY.md section 8e), or with the context's opt-in GPU lane
@@ -117,10 +122,11 @@ class ShardedStream:
     section 8e): callers hash it beside this (host thread) and report it as the Amdahl term.
     """
 
-    def __init__(self, encoder, frames_per_rank: int, dist=None, group=None, device="cpu"):
+    def __init__(self, encoder, frames_per_rank: int, dist=None, group=None, device="cpu", comm=None):
         import torch
 
         self.enc, self.F, self.dist, self.group = encoder, frames_per_rank, dist, group
+        self.comm = comm  # flacgpu.Comm: the gather through the C ABI (GPU encoder only)
         self.world = dist.get_world_size(group) if dist else 1
         self.rank = dist.get_rank(group) if dist else 0
         self.device = torch.device(device)
@@ -169,7 +175,17 @@ class ShardedStream:
             frames = torch.from_numpy(np.frombuffer(fr, dtype=np.uint8).copy()).to(self.device)
             sizes = torch.tensor(sz, dtype=torch.int32, device=self.device)
             nbytes = None
-        if self.dist:
+        if self.gpu and self.comm is not None:
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            r0 = self.rank == 0
+            tb, tf = self.comm.gather_device(frames.data_ptr(), 0, sizes.data_ptr(), self.F,
+                                             d_recv=self.body.data_ptr() if r0 else 0,
+                                             recv_cap=self.body.numel() if r0 else 0,
+                                             d_recv_sizes=self.fsz.data_ptr() if r0 else 0,
+                                             recv_sizes_cap=self.fsz.numel() if r0 else 0,
+                                             d_nbytes=nbytes.data_ptr(), stream=st)
+            got = (self.body[:tb], self.fsz[:tf]) if r0 else None
+        elif self.dist:
             got = gather_frames(self.dist, self.group, frames, sizes, self.rank, self.world, nbytes=nbytes,
                                 recv=(self.body, self.fsz) if self.gpu and self.rank == 0 else None)
         else:
@@ -216,14 +232,39 @@ def _encode_shard(encoder, pcm: bytes, per: int, s0: int, s1: int, f0: int, devi
             torch.tensor(sizes, dtype=torch.int32, device=device))
 
 
-def encode_sharded(encoder, pcm: bytes, dist=None, group=None, device="cpu", md5: str = "host") -> Optional[bytes]:
+def gather_comm(comm, frames, sizes, rank: int):
+    """gather_frames over a flacgpu.Comm (C ABI, RCCL inside libflacgpu.so): device tensors of this
+    rank's frames/sizes -> rank 0 gets (bitstream, sizes) device tensors, others None.  Two gathers:
+    first every rank's (frames, bytes) counts, so that rank 0 can size its receive buffers."""
+    import torch
+
+    st = torch.cuda.current_stream(frames.device).cuda_stream
+    cnt = torch.tensor([sizes.numel(), frames.numel()], dtype=torch.int64, device=frames.device)
+    allc = torch.empty(2 * comm.world, dtype=torch.int64, device=frames.device)
+    comm.gather_device(cnt.data_ptr(), 16, 0, 0, d_recv=allc.data_ptr() if rank == 0 else 0,
+                       recv_cap=16 * comm.world if rank == 0 else 0, stream=st)
+    if rank == 0:
+        c = allc.view(-1, 2).cpu().tolist()
+        body = torch.empty(max(1, sum(x[1] for x in c)), dtype=torch.uint8, device=frames.device)
+        fsz = torch.empty(max(1, sum(x[0] for x in c)), dtype=torch.int32, device=frames.device)
+        tb, tf = comm.gather_device(frames.data_ptr(), frames.numel(), sizes.data_ptr(), sizes.numel(),
+                                    d_recv=body.data_ptr(), recv_cap=body.numel(), d_recv_sizes=fsz.data_ptr(),
+                                    recv_sizes_cap=fsz.numel(), stream=st)
+        return body[:tb], fsz[:tf]
+    comm.gather_device(frames.data_ptr(), frames.numel(), sizes.data_ptr(), sizes.numel(), stream=st)
+    return None
+
+
+def encode_sharded(encoder, pcm: bytes, dist=None, group=None, device="cpu", md5: str = "host",
+                   comm=None) -> Optional[bytes]:
     """Encode one stream (interleaved LE PCM, identical on every rank) across the ranks of
     `group`; returns the whole .flac file on rank 0 and None elsewhere.
 
     `encoder` provides channels, bits, sample_rate, bytes_per_sample, block_size and either
     encode_frames_device(d_pcm, n, first_frame) -> (uint8 tensor, int32 tensor) on a GPU
     (flacgpu.Encoder; frames stay in HBM) or encode_frames(pcm, first_frame) -> (bytes,
-    sizes).  `device` is where the gather's tensors live ("cuda:k" for RCCL, "cpu" for gloo).
+    sizes).  `device` is where the gather's tensors live ("cuda:k" for RCCL, "cpu" for gloo).  `comm` (flacgpu.Comm,
+    GPU encoder): the gather runs through the C ABI instead of torch.distributed.
     """
     import ctypes
 
@@ -248,7 +289,10 @@ def encode_sharded(encoder, pcm: bytes, dist=None, group=None, device="cpu", md5
             digest["md5"] = encoder.md5(pcm)
         finally:
             encoder.set_md5_engine(prev)
-    got = gather_frames(dist, group, frames, sizes, rank, world) if dist else (frames, sizes)
+    if comm is not None:
+        got = gather_comm(comm, frames, sizes, rank)
+    else:
+        got = gather_frames(dist, group, frames, sizes, rank, world) if dist else (frames, sizes)
     if rank != 0:
         return None
     body, fsz = got
