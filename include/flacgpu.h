@@ -319,7 +319,8 @@ typedef struct {
     double device_lane;
     double device_chip;
     int32_t host_workers;
-    int32_t measured; /* 1: host_chain measured in this process; 2: set by the caller */
+    int32_t measured; /* 1: host_chain measured in this process; 2: set by the caller; 3: measured while
+                         other chains were hashing on the pool (possibly low: set_rates(NULL) re-measures) */
 } flacgpu_md5_rates;
 /* The current rates (measures the host ones on first use, ~2 ms).  Needs no GPU. */
 int flacgpu_md5_get_rates(flacgpu_md5_rates *out);
@@ -424,7 +425,8 @@ int flacgpu_reset_timing(flacgpu_ctx *ctx);
 
 /* Decision records (for parity tests): when enabled, each encode call also
  * stores one flacgpu_frame_record per frame, readable with
- * flacgpu_get_records after a synchronous call. */
+ * flacgpu_get_records after a synchronous call (flacgpu_encode_files: the
+ * records of every file, file after file, in frame order). */
 typedef struct {
     uint8_t type;       /* 0 CONSTANT, 1 VERBATIM, 2 FIXED, 3 LPC */
     uint8_t waste;

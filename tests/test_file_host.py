@@ -184,8 +184,16 @@ def test_gpu_encode_files_where_the_pipeline_cannot_run(mode):
         if mode == "records_on":
             enc.set_records(True)
         outs = enc.encode_files(pcms)
+        recs = enc.records() if mode == "records_on" else None
     for i, pcm in enumerate(pcms):
         assert outs[i] == oracle_ref.encode_file(pcm, ch, bits, rate), f"file {i}"
+    if recs is not None:
+        # the records of EVERY file, file after file in frame order, each frame's
+        # size equal to the one the restatement writes
+        nfs = [(n + 4095) // 4096 for n in lens]
+        assert len(recs) == sum(nfs)
+        ref_sizes = [s for pcm in pcms if pcm for s in oracle_ref.encode_stream(pcm, ch, bits, rate)[1]]
+        assert [r.frame_bytes for r in recs] == ref_sizes
 
 
 @pytest.mark.gpu
@@ -316,3 +324,53 @@ def test_host_md5_pool_matches_plain_chain(threads):
     r = subprocess.run([os.path.join(CPP_DIR, "build", "md5_pool_test")], capture_output=True, text=True,
                        env=dict(os.environ, FLACGPU_MD5_THREADS=threads), timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ch,bits,rate", [(2, 16, 44100), (2, 24, 96000)])
+def test_concurrent_encode_file_share_the_device_pipeline(ch, bits, rate, monkeypatch):
+    """flacgpu_encode_file from many threads, one context each (the reference's
+    one-encoder-per-file shape, wav2flac.zig:10-63), runs through the device's shared file pipeline
+    (fg_file.cpp); every file must still be byte-identical to the restatement's whole-file encode,
+    including empty and sub-block files, and a caller with too small an output buffer gets
+    WriteFailed without disturbing the others' files."""
+    import ctypes
+    import threading
+
+    import flacgpu
+
+    lens = [0, 1, 4095, 4096, 3 * 4096 + 7, 20 * 4096 + 333, 9000, 12 * 4096, 5, 2 * 4096 + 1, 40000, 7 * 4096]
+    pcms = [synth.synth_pcm(n, ch, bits, rate, stream=i) for i, n in enumerate(lens)]
+    encs = [flacgpu.Encoder(ch, bits, rate, max_frames=64) for _ in pcms]
+    outs, errs = [None] * len(pcms), [None] * len(pcms)
+    small = 5  # this caller's buffer is too small
+
+    def run(i):
+        try:
+            if i == small:
+                e = encs[i]
+                n = lens[i]
+                out = ctypes.create_string_buffer(100)
+                ol = ctypes.c_size_t(0)
+                errs[i] = e.lib.flacgpu_encode_file(e.ctx, pcms[i], e.bytes_per_sample, n, out, 100, ctypes.byref(ol))
+            else:
+                outs[i] = encs[i].encode_file(pcms[i])
+        except Exception as ex:  # noqa: BLE001
+            errs[i] = ex
+
+    try:
+        for _ in range(2):
+            th = [threading.Thread(target=run, args=(i,)) for i in range(len(pcms))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            assert errs[small] == -4, errs[small]  # FLACGPU_ERR_OUTPUT_TOO_SMALL
+            for i, pcm in enumerate(pcms):
+                if i == small:
+                    continue
+                assert errs[i] is None, errs[i]
+                assert outs[i] == oracle_ref.encode_file(pcm, ch, bits, rate), f"file {i} ({lens[i]} samples)"
+    finally:
+        for e in encs:
+            e.close()

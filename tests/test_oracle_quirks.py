@@ -58,7 +58,7 @@ def test_part_size_no_half_len_at_p0():
 
 
 def rice_closed_form(S, n, maxp):
-    """The GPU kernel's closed-form parameter choice (fg_kernels.hip rice_choose)."""
+    """The GPU kernel's closed-form parameter choice (zig-flac_amd/csrc/fg_device.hpp rice_choose)."""
     if S <= (n + 1) >> 1:
         p = 0
     else:

@@ -17,6 +17,8 @@
 #                                                          AB_ARGS; rows -> gpurun_out/ab_<tag>.txt
 #   tools/gpu.sh stamps <tag>                              phase stamps (build_st: make OUT=build_st
 #                                                          EXTRA=-DFG_STAMPS) for C2 and the wide configs
+#   tools/gpu.sh diagtests <tag>                           the diagnostic-build-only parity tests (fused, k_ana1,
+#                                                          overlapped schedule) against build_diag/libflacgpu.so
 #   tools/gpu.sh cpuplace <tag>                            CPU-baseline legs alone (no GPU) under each thread
 #                                                          placement -> gpurun_out/<tag>_cpu_<place>.json
 #   tools/gpu.sh final  <tag>                              tests + smoke + profiles of every config at
@@ -120,6 +122,15 @@ do_stamps() {
   done
 }
 
+do_diagtests() {
+  FLACGPU_LIB=$REPO/zig-flac_amd/build_diag/libflacgpu.so timeout -k 10 900 python -u -m pytest tests/test_gpu_fused.py \
+    tests/test_gpu_plan.py tests/test_file_host.py -m gpu -x -q --timeout 120 --timeout-method thread \
+    -k "fused or overlapped or one_wave or without_md5" > gpurun_out/${TAG}_diag_pytest.log 2>&1
+  local rc=$?
+  tail -3 gpurun_out/${TAG}_diag_pytest.log
+  return $rc
+}
+
 do_cpuplace() {
   for place in socket0 idle none; do
     timeout -k 10 300 python -u bench.py --cpu-only --cpu-place $place --configs=c5 > gpurun_out/${TAG}_cpu_$place.json 2> gpurun_out/${TAG}_cpu_$place.err ||
@@ -140,6 +151,7 @@ case $CMD in
   ab) do_ab "$@" ;;
   stamps) do_stamps ;;
   cpuplace) do_cpuplace ;;
+  diagtests) do_diagtests ;;
   final)
     do_tests && do_smoke &&
     do_profile ${TAG}_c2 c2 262144 16384 > gpurun_out/${TAG}_prof_c2.log 2>&1 &&

@@ -125,6 +125,7 @@ struct flacgpu_ctx {
     FrameRec *d_records = nullptr;
     unsigned long long *d_stamps = nullptr;
     bool records_on = false;
+    bool records_keep = false;  // encode_files with records: every file's records, concatenated
     bool ana_split = false;  // full-frame analysis in channel halves (fg_device.hpp k_analyze)
     bool pack_split = false;  // full-frame pack in channel halves (fg_packw.hpp k_packw<..., true>)
     uint32_t nt_psplit = 0, lds_psplit = 0, image_split = 0, crc_hmaxs = 0;
@@ -572,6 +573,7 @@ int fg::ctx_download_chunk(flacgpu_ctx *c, uint8_t *out, uint64_t total) {
 }
 
 uint32_t fg::ctx_max_frames(const flacgpu_ctx *c) { return c->max_frames; }
+bool fg::ctx_plain(const flacgpu_ctx *c) { return !c->records_on && !c->timing && c->ovl_chunks <= 1 && !c->fused; }
 fg::CtxDevice fg::ctx_device(const flacgpu_ctx *c) {
     return {c->device, (void *)c->stream, c->d_out, c->d_fbytes, c->d_total, c->out_cap, c->C, c->B,
             c->cfg.block_size};
@@ -1068,14 +1070,20 @@ int fg::ctx_encode_segments(flacgpu_ctx *c, uint32_t n, const uint8_t *const *sr
     // flacgpu_encode_file does for them
     auto one_by_one = [&]() -> int {
         for (uint32_t i = 0; i < n; i++) out_len[i] = 0;
+        // with decision records on, the records of EVERY file are kept, file after file in frame
+        // order (flacgpu_get_records), not only the last file's
+        if (c->records_on) c->h_records.clear();
+        c->records_keep = true;
         for (uint32_t i = 0; i < n; i++) {
             const int r = flacgpu_encode_frames(c, src[i], c->B, n_samples[i], 0, out[i], out_cap[i], &out_len[i],
                                                 frame_bytes ? frame_bytes[i] : nullptr);
             if (r) {
+                c->records_keep = false;
                 for (uint32_t j = 0; j < n; j++) out_len[j] = 0;
                 return r;
             }
         }
+        c->records_keep = false;
         return FLACGPU_OK;
     };
     if (c->max_frames < c->pipe_sets || c->records_on) return one_by_one();
@@ -1115,7 +1123,7 @@ int flacgpu_encode_frames(flacgpu_ctx *c, const void *pcm, uint32_t bytes_per_sa
     const uint8_t *src = (const uint8_t *)pcm;
     uint64_t frame0 = 0;
     size_t written = 0;
-    if (c->records_on) c->h_records.clear();
+    if (c->records_on && !c->records_keep) c->h_records.clear();
     if (!c->records_on && c->max_frames >= c->pipe_sets &&
         total_frames > std::min<uint64_t>(c->max_frames / c->pipe_sets, 2048u)) {
         PipeSeg seg{src, n_samples, first_frame_number, out, out_cap, 0, frame_bytes};
@@ -1360,11 +1368,11 @@ static flacgpu_md5_rates md5_rates() {
     std::lock_guard<std::mutex> lk(g_rates_mu);
     if (!g_rates_set) {
         flacgpu_md5_rates r{};
-        fg::md5_measure_rates(r.host_chain, r.host_chains);
+        const bool contended = fg::md5_measure_rates(r.host_chain, r.host_chains);
         r.device_lane = 72e6;
         r.device_chip = 600e9;
         r.host_workers = fg::md5_pool_workers();
-        r.measured = 1;
+        r.measured = contended ? 3 : 1;
         g_rates = r;
         g_rates_set = true;
     }
@@ -1378,23 +1386,22 @@ int flacgpu_md5_get_rates(flacgpu_md5_rates *out) {
 }
 
 int flacgpu_md5_set_rates(const flacgpu_md5_rates *r) {
+    // the whole struct is validated on a local copy first: a rejected call leaves the rates in use
+    // (measured or set earlier) as they were
+    flacgpu_md5_rates v{};
     if (r) {
-        for (double v : r->host_chain)
-            if (!(v > 0)) return FLACGPU_ERR_INVALID_INPUT;
-        if (!(r->device_lane > 0) || !(r->device_chip > 0) || r->host_workers < 0) return FLACGPU_ERR_INVALID_INPUT;
+        v = *r;
+        for (double x : v.host_chain)
+            if (!(x > 0)) return FLACGPU_ERR_INVALID_INPUT;
+        if (!(v.device_lane > 0) || !(v.device_chip > 0) || v.host_workers < 0) return FLACGPU_ERR_INVALID_INPUT;
+        if (!v.host_chains[0])
+            for (uint32_t i = 0; i < 4; i++) v.host_chains[i] = i + 1u;
+        for (uint32_t i = 1; i < 4; i++)
+            if (v.host_chains[i] <= v.host_chains[i - 1]) return FLACGPU_ERR_INVALID_INPUT;
+        v.measured = 2;
     }
     std::lock_guard<std::mutex> lk(g_rates_mu);
-    if (r) {
-        g_rates = *r;
-        g_rates.measured = 2;
-        if (!g_rates.host_chains[0])
-            for (uint32_t i = 0; i < 4; i++) g_rates.host_chains[i] = i + 1u;
-        for (uint32_t i = 1; i < 4; i++)
-            if (g_rates.host_chains[i] <= g_rates.host_chains[i - 1]) {
-                g_rates_set = false;
-                return FLACGPU_ERR_INVALID_INPUT;
-            }
-    }
+    if (r) g_rates = v;
     g_rates_set = r != nullptr;
     return FLACGPU_OK;
 }

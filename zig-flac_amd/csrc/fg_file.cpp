@@ -7,10 +7,16 @@
 // GPU kernels via flacgpu_encode_frames; only the 73 metadata bytes are built
 // here.
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
 #include <system_error>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/flacgpu.h"
@@ -27,6 +33,117 @@ uint32_t rd_le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8
 uint16_t rd_le16(const uint8_t *p) { return (uint16_t)(p[0] | p[1] << 8); }
 void wr_be(uint8_t *p, uint64_t v, int n) {
     for (int i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * (n - 1 - i)));
+}
+
+// ---- The device's shared file pipeline --------------------------------------------------
+// The reference converts one file per encoder (wav2flac.zig:10-63).  Many such encoders on one GPU,
+// each with its own streams and chunk pipeline, contend for the device's few hardware queues
+// (GPU_MAX_HW_QUEUES = 4) and each launch their persistent grids over a small chunk: 64 concurrent
+// flacgpu_encode_file calls ran at 0.25 of the host-MD5 bound.  So a
+// flacgpu_encode_file call on a plain context (fg::ctx_plain) with the host MD5 engine queues its
+// file on the shared pipeline of (device, config): one caller at a time is the leader and runs
+// every file queued by then as ONE flacgpu_encode_files batch on the pipeline's own context (one
+// H2D / encode / D2H schedule running on from file to file, all MD5s on the host pool); the other
+// callers wait for their file and take over as leader when the batch ends.  Output bytes are those
+// of flacgpu_encode_file (flacgpu_encode_files' contract).  FLACGPU_FILE_SHARED=0 turns it off.
+struct FileReq {
+    const void *pcm;
+    uint64_t n;
+    uint8_t *out;
+    size_t cap, len = 0;
+    int rc = FLACGPU_OK;
+    bool done = false;
+};
+
+struct FilePipe {
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<FileReq *> q;
+    bool leading = false;
+    flacgpu_ctx *ctx = nullptr;  // opened by the first leader, kept for the process lifetime
+    int open_rc = FLACGPU_OK;
+};
+
+constexpr uint32_t kPipeFrames = 6144;  // three 2048-frame chunk sets (the pipelined schedule)
+
+FilePipe &file_pipe(int device, const flacgpu_config &c) {
+    static std::mutex mm;
+    static std::map<std::tuple<int, uint32_t, uint32_t, uint32_t, uint32_t>, FilePipe *> pipes;
+    const auto key = std::make_tuple(device, c.sample_rate, (uint32_t)c.block_size | ((uint32_t)c.channels << 16) |
+                                                                ((uint32_t)c.bits_per_sample << 24),
+                                     (uint32_t)c.stereo_decorrelation | ((uint32_t)c.max_rice_part_order << 8) |
+                                         ((uint32_t)c.max_rice_param << 16),
+                                     (uint32_t)c.prediction);
+    std::lock_guard<std::mutex> lk(mm);
+    FilePipe *&p = pipes[key];
+    if (!p) p = new FilePipe;  // never freed: callers may still hold it at exit
+    return *p;
+}
+
+bool file_pipe_on() {
+    const char *e = std::getenv("FLACGPU_FILE_SHARED");
+    return !(e && e[0] == '0');
+}
+
+// Queue one file on the shared pipeline and return when it is encoded (maybe by another caller).
+int file_pipe_encode(int device, const flacgpu_config &cfg, const void *pcm, uint32_t bytes_per_sample, uint64_t n,
+                     uint8_t *out, size_t cap, size_t *out_len) {
+    FilePipe &P = file_pipe(device, cfg);
+    FileReq me{pcm, n, out, cap};
+    std::unique_lock<std::mutex> lk(P.m);
+    P.q.push_back(&me);
+    P.cv.notify_all();
+    for (;;) {
+        P.cv.wait(lk, [&] { return me.done || !P.leading; });
+        if (me.done) break;
+        // no batch running and this file still queued: lead.  Give callers that start at the same
+        // moment a short window to queue theirs (the batch grows while the queue keeps growing)
+        P.leading = true;
+        for (int i = 0; i < 20; i++) {
+            const size_t before = P.q.size();
+            P.cv.wait_for(lk, std::chrono::microseconds(100));
+            if (P.q.size() == before) break;
+        }
+        std::vector<FileReq *> batch(P.q.begin(), P.q.end());
+        P.q.clear();
+        lk.unlock();
+        int rc = FLACGPU_OK;
+        if (!P.ctx && P.open_rc == FLACGPU_OK) P.open_rc = flacgpu_open(device, &cfg, kPipeFrames, &P.ctx);
+        rc = P.ctx ? FLACGPU_OK : (P.open_rc ? P.open_rc : FLACGPU_ERR_DEVICE);
+        const uint32_t nb = (uint32_t)batch.size();
+        std::vector<const void *> src(nb);
+        std::vector<uint64_t> ns(nb);
+        std::vector<uint8_t *> outs(nb);
+        std::vector<size_t> caps(nb), lens(nb, 0);
+        for (uint32_t i = 0; i < nb; i++) {
+            src[i] = batch[i]->pcm;
+            ns[i] = batch[i]->n;
+            outs[i] = batch[i]->out;
+            caps[i] = batch[i]->cap;
+        }
+        if (!rc) rc = flacgpu_encode_files(P.ctx, nb, src.data(), bytes_per_sample, ns.data(), outs.data(), caps.data(),
+                                           lens.data());
+        if (rc == FLACGPU_ERR_OUTPUT_TOO_SMALL || rc == FLACGPU_ERR_INVALID_INPUT) {
+            // one file's buffer is too small (or its pointer bad): every file of the batch alone,
+            // so that each caller gets its own file's result
+            for (uint32_t i = 0; i < nb; i++) {
+                size_t l = 0;
+                batch[i]->rc = flacgpu_encode_files(P.ctx, 1, &src[i], bytes_per_sample, &ns[i], &outs[i], &caps[i], &l);
+                batch[i]->len = l;
+            }
+        } else {
+            for (uint32_t i = 0; i < nb; i++) {
+                batch[i]->rc = rc;
+                batch[i]->len = rc ? 0 : lens[i];
+            }
+        }
+        lk.lock();
+        for (FileReq *r : batch) r->done = true;
+        P.leading = false;
+        P.cv.notify_all();
+    }
+    *out_len = me.len;
+    return me.rc;
 }
 
 }  // namespace
@@ -147,7 +264,8 @@ size_t flacgpu_vorbis_comment_bytes(int last_metadata, uint8_t out[31]) {
     return 12 + kVendorLen;
 }
 
-// wav2flac.main + encode (wav2flac.zig:10-97) for PCM already in memory: skipHeader,
+// wav2flac.main + encode (wav2flac.zig:10-97) for PCM already in memory (on a plain context with
+// the host MD5 engine: through the device's shared file pipeline above): skipHeader,
 // writeVorbisComment(true), every frame through the GPU (sizes replayed into
 // updateFrameSize in frame order), the MD5 of the PCM bytes, then the header written
 // last.  With the host MD5 engine (the default) the hash runs on its own thread while
@@ -162,6 +280,9 @@ int flacgpu_encode_file(flacgpu_ctx *ctx, const void *pcm, uint32_t bytes_per_sa
     if (rc) return rc;
     if (out_cap < 73) return FLACGPU_ERR_OUTPUT_TOO_SMALL;
     if (bytes_per_sample != cfg.bits_per_sample / 8u) return FLACGPU_ERR_INVALID_INPUT;
+    if (flacgpu_md5_get_engine(ctx) == FLACGPU_MD5_HOST && fg::ctx_plain(ctx) && file_pipe_on())
+        return file_pipe_encode(fg::ctx_device(ctx).device, cfg, pcm, bytes_per_sample, n_samples, out, out_cap,
+                                out_len);
     const uint64_t block = cfg.block_size;
     const uint64_t n_frames = (n_samples + block - 1) / block;
     const size_t pcm_bytes = (size_t)(n_samples * cfg.channels * bytes_per_sample);

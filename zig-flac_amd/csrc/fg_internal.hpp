@@ -32,5 +32,9 @@ struct CtxDevice {
     uint32_t channels, bytes_per_sample, block_size;
 };
 CtxDevice ctx_device(const flacgpu_ctx *c);
+// The context runs the default schedule with no per-context instrumentation (no decision
+// records, no kernel timing, no diagnostic schedule): its host-buffer file work may then run on
+// the device's shared file pipeline (fg_file.cpp) instead of on its own streams.
+bool ctx_plain(const flacgpu_ctx *c);
 void ctx_finish(flacgpu_ctx *c);  // fold pending timing events
 }  // namespace fg

@@ -379,6 +379,11 @@ class Md5Pool {
         for (auto &j : jobs) j.h->update(j.tail, j.tail_len);
     }
     int workers() const { return workers_; }
+    // chains held by workers or queued (other callers hashing right now)
+    bool busy() {
+        std::lock_guard<std::mutex> lk(m_);
+        return active_ > 0 || !q_.empty();
+    }
 
   private:
     // up to four chains interleaved per worker: a core's throughput is flat past ~4 chains and
@@ -524,12 +529,14 @@ bool md5_avx512() { return avx512_on(); }
 // caches: the pool's chains stream from memory, but MD5 at ~1 GB/s per chain is far below what a
 // core can fetch), so SMT siblings, the workers' placement and wake-up costs are in the figure;
 // best of three per point, ~5-15 ms in all.  Without a pool: one chain on the caller.
-void md5_measure_rates(double rate[4], uint32_t pts[4]) {
-    constexpr size_t kLen = 256 * 1024;
+bool md5_measure_rates(double rate[4], uint32_t pts[4]) {
+    // chain j hashes 256 KiB slice j mod 128 of a 32-MiB buffer: streaming reads, as a real
+    // file's chain does, not one cache-resident block re-read by every chain
+    constexpr size_t kLen = 256 * 1024, kSlices = 128;
     static uint8_t *buf = [] {
-        uint8_t *b = new uint8_t[kLen];
+        uint8_t *b = new uint8_t[kLen * kSlices];
         uint32_t x = 0x12345678u;
-        for (size_t i = 0; i < kLen; i++) {
+        for (size_t i = 0; i < kLen * kSlices; i++) {
             x = x * 1664525u + 1013904223u;
             b[i] = (uint8_t)(x >> 24);
         }
@@ -538,16 +545,27 @@ void md5_measure_rates(double rate[4], uint32_t pts[4]) {
     Md5Pool &pool = Md5Pool::get();
     const int W = pool.workers();
     const bool vec = avx512_on();  // points past four chains per worker use the vector path
+    bool contended = false;
     for (int i = 0; i < 4; i++) pts[i] = vec ? (i == 0 ? 1u : 4u << (i - 1)) : (uint32_t)(i + 1);
     for (int i = 0; i < 4; i++) {
         const size_t n = W > 0 ? (size_t)pts[i] * W : 1;
         std::vector<HostMd5> hs(n);
         std::vector<HostMd5 *> hp(n);
-        std::vector<const uint8_t *> ps(n, buf);
+        std::vector<const uint8_t *> ps(n);
         std::vector<size_t> lens(n, kLen);
-        for (size_t j = 0; j < n; j++) hp[j] = &hs[j];
+        for (size_t j = 0; j < n; j++) {
+            hp[j] = &hs[j];
+            ps[j] = buf + (j % kSlices) * kLen;
+        }
         double best = 0;
         for (int rep = 0; rep < 3; rep++) {
+            // another caller's chains on the pool would share its workers with this sample: wait
+            // (up to 50 ms) for the pool to drain; a sample that still overlaps them is reported
+            // as contended (flacgpu_md5_rates.measured = 3)
+            if (W > 0) {
+                for (int t = 0; t < 50 && pool.busy(); t++) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                contended |= pool.busy();
+            }
             const auto t0 = std::chrono::steady_clock::now();
             if (W > 0) pool.run_many(hp.data(), ps.data(), lens.data(), n);
             else hs[0].update(buf, kLen);
@@ -560,6 +578,7 @@ void md5_measure_rates(double rate[4], uint32_t pts[4]) {
             break;
         }
     }
+    return contended;
 }
 
 void HostMd5::reset() {

@@ -45,7 +45,8 @@ int md5_pool_workers();
 
 // measured host MD5 rates: bytes/s per pool worker with pts[i] chains each (pts: 1, 2, 3, 4; with
 // the AVX-512 path 1, 4, 8, 16); no pool: one chain's rate on the caller in every entry
-void md5_measure_rates(double rate[4], uint32_t pts[4]);
+// true if other chains were on the pool during the measurement (the rates may be low)
+bool md5_measure_rates(double rate[4], uint32_t pts[4]);
 
 // the AVX-512 sixteen-chain MD5 is in use (host support, FLACGPU_MD5_AVX512 != 0)
 bool md5_avx512();
