@@ -19,6 +19,8 @@
 #                                                          EXTRA=-DFG_STAMPS) for C2 and the wide configs
 #   tools/gpu.sh diagtests <tag>                           the diagnostic-build-only parity tests (fused, k_ana1,
 #                                                          overlapped schedule) against build_diag/libflacgpu.so
+#   tools/gpu.sh e2e <tag> <threads...>                    tools/e2e_probe.py once per host MD5 pool size
+#                                                          -> gpurun_out/<tag>_e2e_<threads>.json
 #   tools/gpu.sh cpuplace <tag>                            CPU-baseline legs alone (no GPU) under each thread
 #                                                          placement -> gpurun_out/<tag>_cpu_<place>.json
 #   tools/gpu.sh final  <tag>                              tests + smoke + profiles of every config at
@@ -131,6 +133,15 @@ do_diagtests() {
   return $rc
 }
 
+do_e2e() {
+  for t in "$@"; do
+    FLACGPU_MD5_THREADS=$t timeout -k 10 400 python -u tools/e2e_probe.py --e2e-files ${E2E_FILES:-32,64} \
+      --e2e-many ${E2E_MANY:-256} > gpurun_out/${TAG}_e2e_$t.json 2> gpurun_out/${TAG}_e2e_$t.err ||
+      { tail -5 gpurun_out/${TAG}_e2e_$t.err; return 1; }
+    tail -1 gpurun_out/${TAG}_e2e_$t.json
+  done
+}
+
 do_cpuplace() {
   for place in socket0 idle none; do
     timeout -k 10 300 python -u bench.py --cpu-only --cpu-place $place --configs=c5 > gpurun_out/${TAG}_cpu_$place.json 2> gpurun_out/${TAG}_cpu_$place.err ||
@@ -151,6 +162,7 @@ case $CMD in
   ab) do_ab "$@" ;;
   stamps) do_stamps ;;
   cpuplace) do_cpuplace ;;
+  e2e) do_e2e "$@" ;;
   diagtests) do_diagtests ;;
   final)
     do_tests && do_smoke &&

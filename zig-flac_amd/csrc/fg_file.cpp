@@ -96,13 +96,16 @@ int file_pipe_encode(int device, const flacgpu_config &cfg, const void *pcm, uin
     for (;;) {
         P.cv.wait(lk, [&] { return me.done || !P.leading; });
         if (me.done) break;
-        // no batch running and this file still queued: lead.  Give callers that start at the same
-        // moment a short window to queue theirs (the batch grows while the queue keeps growing)
+        // no batch running and this file still queued: lead.  Give callers that start at about the
+        // same moment a window to queue theirs: the batch closes once no file has arrived for 1 ms
+        // (at most 20 ms; a batch of ten-minute files runs for ~100 ms, and every file left out of
+        // it waits for the whole next batch)
         P.leading = true;
-        for (int i = 0; i < 20; i++) {
+        const auto t_lead = std::chrono::steady_clock::now();
+        for (;;) {
             const size_t before = P.q.size();
-            P.cv.wait_for(lk, std::chrono::microseconds(100));
-            if (P.q.size() == before) break;
+            P.cv.wait_for(lk, std::chrono::milliseconds(1), [&] { return P.q.size() != before; });
+            if (P.q.size() == before || std::chrono::steady_clock::now() - t_lead > std::chrono::milliseconds(20)) break;
         }
         std::vector<FileReq *> batch(P.q.begin(), P.q.end());
         P.q.clear();
