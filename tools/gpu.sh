@@ -136,7 +136,7 @@ do_diagtests() {
 do_e2e() {
   for t in "$@"; do
     FLACGPU_MD5_THREADS=$t timeout -k 10 400 python -u tools/e2e_probe.py --e2e-files ${E2E_FILES:-32,64} \
-      --e2e-many ${E2E_MANY:-256} > gpurun_out/${TAG}_e2e_$t.json 2> gpurun_out/${TAG}_e2e_$t.err ||
+      --e2e-many ${E2E_MANY:-256} $E2E_ARGS > gpurun_out/${TAG}_e2e_$t.json 2> gpurun_out/${TAG}_e2e_$t.err ||
       { tail -5 gpurun_out/${TAG}_e2e_$t.err; return 1; }
     tail -1 gpurun_out/${TAG}_e2e_$t.json
   done

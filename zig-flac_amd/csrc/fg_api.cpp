@@ -87,7 +87,8 @@ struct TimedLaunch {
 // to wait for the encode of chunk i-2 and the encode for the download of chunk i-2, so a slow
 // download or a late host thread stalled both directions of PCIe (round-4 batches reached 33-44 GB/s
 // of H2D against 57 GB/s measured alone)
-constexpr uint32_t kPipeSets = 3;  // the most; flacgpu_ctx::pipe_sets is the number in use (2 or 3)
+constexpr uint32_t kPipeSets = 4;  // the most; flacgpu_ctx::pipe_sets is the number in use (2..4)
+constexpr uint32_t kPipeSetsDefault = 3;
 
 struct flacgpu_ctx {
     int device = 0;
@@ -103,7 +104,7 @@ struct flacgpu_ctx {
     hipEvent_t up_done[kPipeSets] = {};  // a chunk set's upload landed (GPU-side waits)
     hipEvent_t set_done[kPipeSets] = {};  // a chunk set's encode finished (GPU-side waits)
     hipEvent_t dl_done[kPipeSets] = {};   // a chunk set's frames downloaded (GPU-side waits)
-    uint32_t pipe_sets = kPipeSets;  // chunk sets in use (FLACGPU_PIPE_SETS = 2: the round-4 schedule)
+    uint32_t pipe_sets = kPipeSetsDefault;  // chunk sets in use (FLACGPU_PIPE_SETS = 2: the round-4 schedule; 4)
     hipEvent_t fork = nullptr, join = nullptr;
     // host waits of the pipelined host-buffer path (the download stream, the end; the chunk sets'
     // own events are set_done below):
@@ -701,10 +702,15 @@ int flacgpu_open(int device, const flacgpu_config *cfg, uint32_t max_frames_per_
     if (const char *e = std::getenv("FLACGPU_XCD_QUEUE")) c->xcd_queue = e[0] != '0';
     if (const char *e = std::getenv("FLACGPU_PACK_XCDQ")) c->pack_xcdq = e[0] != '0';
     if (const char *e = std::getenv("FLACGPU_SPLIT_JIT")) c->split_jit = (uint32_t)std::atoi(e) & 3u;
-    if (const char *e = std::getenv("FLACGPU_PIPE_SETS")) c->pipe_sets = e[0] == '2' ? 2u : kPipeSets;
+    if (const char *e = std::getenv("FLACGPU_PIPE_SETS")) {
+        const int v = std::atoi(e);
+        c->pipe_sets = v >= 2 && v <= (int)kPipeSets ? (uint32_t)v : kPipeSetsDefault;
+    }
+    // issue priority of the stream-MD5 waves (output-invariant): 1 trades 2-5 % of the encode for a
+    // 35-58 % shorter MD5 chain -- for a workload whose MD5 would bind the step
+    if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e) ? 1 : 0;
 #if FG_DIAG
-    // diagnostic build only: issue priorities, grid reserves, the overlapped schedule's shape
-    if (const char *e = std::getenv("FLACGPU_MD5_PRIO")) c->md5_prio = std::atoi(e);
+    // diagnostic build only: grid reserves, the overlapped schedule's shape
     if (const char *e = std::getenv("FLACGPU_ENC_PRIO")) c->enc_prio = e[0] == '1' ? 1u : 0u;
     if (const char *e = std::getenv("FLACGPU_MD5_RESERVE")) c->md5_reserve = std::atoi(e);
     if (const char *e = std::getenv("FLACGPU_MD5_DIAG")) c->md5_prio |= std::atoi(e) << 8;

@@ -110,11 +110,6 @@ __device__ __forceinline__ T dppT(T v, int which);
 #ifndef FG_MAX
 #define FG_MAX(a, b) max((a), (b))
 #endif
-// the frame CRC-16 patched into the last store unit(s) (store_frame16_crc) instead of written into the
-// image by thread 0 between two barriers (A/B switch)
-#ifndef FG_CRC_PATCH
-#define FG_CRC_PATCH 1
-#endif
 // LKEEP for 24-bit LPC frames (c3): the fast pass's residuals kept for the exact pass (A/B switch)
 #ifndef FG_LKEEP24
 #define FG_LKEEP24 1
@@ -338,75 +333,6 @@ __device__ __forceinline__ void store_frame16(const uint32_t *img, uint8_t *out,
                 for (uint32_t b = 0; b < 4; b++) {
                     const uint64_t bb = b0 + 4u * c + b;
                     if (bb >= DL && bb < E) out[bb] = (uint8_t)(v[c] >> (8 * b));
-                }
-        }
-    }
-}
-
-// The frame's CRC-16 (frame_writer.zig:144-148) from the workgroup's per-wave partials misc[0..NW)
-// (residue mod Q and parity of each wave's words, XOR-reduced) plus the < 4 bytes past the last
-// whole word W4 (bytes W4*4 .. Lb-1 of the image).
-__device__ __forceinline__ uint32_t frame_crc(const uint32_t *misc, uint32_t NW, const uint32_t *img, uint32_t W4,
-                                              uint32_t Lb) {
-    uint32_t qp = 0;
-    for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
-    uint32_t crc = crc_from_q(qp);
-    for (uint32_t b = W4 * 4u; b < Lb; b++) crc = crc_byte_v(crc, (img[b >> 2] >> (24 - 8 * (b & 3))) & 255u);
-    return crc;
-}
-
-// store_frame16 of a frame whose last two bytes (frame bytes Lb, Lb + 1 = fbytes - 2, fbytes - 1)
-// are its CRC-16, still zero in the image: the thread(s) whose 16-B unit holds them compute the CRC
-// from the per-wave partials (frame_crc) and patch it into their unit.  So the stores follow the
-// partials' barrier directly -- no single-thread section and no second barrier between the CRC
-// reduction and the stores.
-__device__ __forceinline__ void store_frame16_crc(const uint32_t *img, uint8_t *out, uint64_t D, uint32_t fbytes,
-                                                  uint32_t tid, uint32_t NT, const uint32_t *misc, uint32_t NW,
-                                                  uint32_t W4) {
-    const uint64_t E = D + fbytes;
-    const uint32_t sa = (uint32_t)(D & 3u);
-    const uint64_t qD = D >> 2;
-    const uint32_t r = (uint32_t)(qD & 3u);
-    const uint64_t cpos = E - 2u;  // the CRC's first byte in out
-    for (uint64_t u = (D >> 4) + tid; u < ((E + 15u) >> 4); u += NT) {
-        const int32_t m0 = (int32_t)(4u * u - qD);
-        const int32_t a1 = m0 + (int32_t)r;
-        const uint4 q1 = *(const uint4 *)(img + a1);
-        const uint4 q0 = a1 >= 4 ? *(const uint4 *)(img + a1 - 4) : make_uint4(0, 0, 0, 0);
-        const uint32_t w8[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-        uint32_t wv[5];
-#pragma unroll
-        for (int c = 0; c < 5; c++)
-            wv[c] = r == 0 ? w8[3 + c] : r == 1 ? w8[2 + c] : r == 2 ? w8[1 + c] : w8[c];
-        uint32_t v[4];
-        uint32_t prev = m0 >= 1 ? wv[0] : 0u;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const uint32_t lo = m0 + c >= 0 ? wv[c + 1] : 0u;
-            v[c] = __builtin_bswap32(sa ? __builtin_amdgcn_alignbyte(prev, lo, sa) : lo);
-            prev = lo;
-        }
-        const uint64_t b0 = 16u * u;
-        if (b0 + 16u > cpos && b0 < cpos + 2u) {  // this unit holds a CRC byte (the last one or two units)
-            const uint32_t crc = frame_crc(misc, NW, img, W4, fbytes - 2u);
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-#pragma unroll
-                for (uint32_t b = 0; b < 4; b++) {
-                    const uint64_t bb = b0 + 4u * c + b;
-                    if (bb == cpos) v[c] |= (crc >> 8) << (8u * b);
-                    else if (bb == cpos + 1u) v[c] |= (crc & 255u) << (8u * b);
-                }
-        }
-        if (b0 >= D && b0 + 16u <= E) {
-            *(uint4 *)(out + b0) = make_uint4(v[0], v[1], v[2], v[3]);
-        } else {
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-#pragma unroll
-                for (uint32_t b = 0; b < 4; b++) {
-                    const uint64_t bb = b0 + 4u * c + b;
-                    if (bb >= D && bb < E) out[bb] = (uint8_t)(v[c] >> (8 * b));
                 }
         }
     }
@@ -2957,11 +2883,6 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
             if (l == 0) misc[wave] = contrib;
         }
         bar_lds();
-#if FG_CRC_PATCH
-        STAMP(5);
-        // ---- 5. image -> out[D, D + fbytes), the CRC-16 patched in by the unit(s) holding it
-        store_frame16_crc(img, a.out, D, fbytes, tid, NT, misc, NW, W4);
-#else
         if (tid == 0) {
             uint32_t qp = 0;
             for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
@@ -2971,9 +2892,10 @@ __global__ void __launch_bounds__(MAXT, ((CLS != 32 && FULL && LPW == 0) ? FG_PA
             put_bits(img, Lb * 8u, crc, 16);
         }
         bar_lds();
+
         STAMP(5);
+        // ---- 5. image -> out[D, D + fbytes)
         store_frame16(img, a.out, D, fbytes, tid, NT);
-#endif
         // the image / staging area is reused by the next frame: with double buffering it is next
         // written by the DMA issued after the next frame's top barrier, which orders these reads
         // before it; synchronous staging refills it before that barrier

@@ -344,12 +344,6 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
             if (l == 0) misc[wave] = contrib;
         }
         bar_lds();
-#if FG_CRC_PATCH
-        STAMP(5);
-        // ---- 5. image -> out[D, D + fbytes), the CRC-16 patched in by the unit(s) holding it
-        // (store_frame16_crc: no thread-0 section and no barrier between the partials and the stores)
-        store_frame16_crc(img, a.out, D, fbytes, tid, NT, misc, NW, W4);
-#else
         if (tid == 0) {
             uint32_t qp = 0;
             for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
@@ -360,8 +354,9 @@ __global__ void __launch_bounds__(MAXT, FG_PACK4_MINW) k_pack4(EncodeArgs a) {
         }
         bar_lds();
         STAMP(5);
+
+        // ---- 5. image -> out[D, D + fbytes)
         store_frame16(img, a.out, D, fbytes, tid, NT);
-#endif
         // no barrier here: the image / staging area is next written by the DMA issued after the
         // next frame's top barrier, which already orders this frame's last reads before it
         STAMP(6);

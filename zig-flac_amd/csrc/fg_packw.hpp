@@ -514,11 +514,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
         }
         bar_lds();
         if (!SPLIT) {
-#if FG_CRC_PATCH
-            STAMP(5);
-            // ---- 5. image -> out[D, D + fbytes), the CRC-16 patched in by the unit(s) holding it
-            store_frame16_crc(img, a.out, D, fbytes, tid, NT, misc, NW, W4);
-#else
             if (tid == 0) {
                 uint32_t qp = 0;
                 for (uint32_t i = 0; i < NW; i++) qp ^= misc[i];
@@ -529,8 +524,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 8)
             }
             bar_lds();
             STAMP(5);
+
+            // ---- 5. image -> out[D, D + fbytes)
             store_frame16(img, a.out, D, fbytes, tid, NT);
-#endif
         } else if (wave == 0) {
             // ---- 4b. this half's CRC partial (half 0: shifted past the bytes after its image)
             uint32_t qp = 0;
