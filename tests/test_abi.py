@@ -136,3 +136,41 @@ def test_release_library_ignores_diagnostic_knobs():
     for knob in ("FLACGPU_FILES_MD5", "FLACGPU_FUSED", "FLACGPU_ANA1", "FLACGPU_OVERLAP", "FLACGPU_ENC_PRIO",
                  "FLACGPU_MD5_RESERVE", "FLACGPU_SPIN_SYNC"):
         assert knob not in strings, knob
+
+
+def _gpu_present():
+    try:
+        import torch
+
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+def test_comm_unique_id_and_argument_checks():
+    """The multi-rank C ABI (fg_comm.cpp): librccl.so.1 opens without a GPU, the communicator id is
+    128 fresh bytes per call, and malformed calls are rejected before any collective."""
+    import ctypes
+
+    a, b = flacgpu.Comm.unique_id(), flacgpu.Comm.unique_id()
+    assert len(a) == len(b) == flacgpu.Comm.ID_BYTES and a != b
+    L = flacgpu.load_library()
+    out = ctypes.c_void_p()
+    cid = (ctypes.c_uint8 * 128).from_buffer_copy(a)
+    for world, rank, dev in ((0, 0, 0), (2, 2, 0), (1, -1, 0), (1, 0, -1)):
+        assert L.flacgpu_comm_init(cid, world, rank, dev, ctypes.byref(out)) == -2, (world, rank, dev)
+    assert L.flacgpu_comm_init(None, 1, 0, 0, ctypes.byref(out)) == -2
+    assert L.flacgpu_comm_rank(None) == -2 and L.flacgpu_comm_size(None) == -2
+    tb, tf = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    assert L.flacgpu_gather_frames_device(None, None, 0, None, None, 0, None, 0, None, 0, ctypes.byref(tb),
+                                          ctypes.byref(tf), None) == -2
+    n = ctypes.c_size_t(0)
+    assert L.flacgpu_encode_frames_sharded(None, None, None, 2, 0, 0, None, 0, ctypes.byref(n), None) == -2
+    L.flacgpu_comm_destroy(None)  # a no-op
+
+
+@pytest.mark.skipif(_gpu_present(), reason="checks the no-device failure path")
+def test_comm_init_fails_loudly_without_gpu():
+    with pytest.raises(flacgpu.FlacGpuError) as e:
+        flacgpu.Comm(flacgpu.Comm.unique_id(), 1, 0, 0)
+    assert e.value.code == -5  # DeviceError, never a CPU fallback
