@@ -601,6 +601,12 @@ static unsigned calc_waste(int64_t *s, uint32_t n, unsigned bps) {
     return w;
 }
 
+/* Analysis mode, NOT the contract (tools/lpc_ratio.py only): every order 1..Q whose coefficients
+ * quantise gets the Rice search and the smallest total wins (an exhaustive order search, what
+ * libFLAC's -e does), to measure what step 7's single order costs in compression. */
+static int g_lpc_exhaustive = 0;
+void oracle_set_lpc_exhaustive(int on) { g_lpc_exhaustive = on != 0; }
+
 /* LPC order search (build-defined, contract above).  Replaces the current
  * choice when an order's total is strictly smaller. */
 static void lpc_search(sub_t *sub, const int64_t *s, uint32_t n, const oracle_config *cfg, unsigned bps,
@@ -632,10 +638,18 @@ static void lpc_search(sub_t *sub, const int64_t *s, uint32_t n, const oracle_co
     }
     if (qs == 0) return;
     int32_t *e = (int32_t *)malloc(n * sizeof(int32_t));
-    /* step 8: the selected order only */
-    for (unsigned q = qs; q == qs; q++) {
-        const int32_t *c = cs;
-        const int shift = shs;
+    /* step 8: the selected order only (analysis mode: every order that quantises) */
+    const unsigned q0 = g_lpc_exhaustive ? 1u : qs, q1 = g_lpc_exhaustive ? (unsigned)valid : qs;
+    for (unsigned q = q0; q <= q1; q++) {
+        int32_t cq[ORACLE_LPC_MAX_ORDER];
+        int shq = shs;
+        if (q != qs) {
+            if (oracle_lpc_quantize(coefs + (q - 1) * ORACLE_LPC_MAX_ORDER, q, ORACLE_LPC_PRECISION, cq, &shq)) continue;
+        } else {
+            memcpy(cq, cs, q * sizeof(int32_t));
+        }
+        const int32_t *c = cq;
+        const int shift = shq;
         if (lpc_residuals(s, n, q, c, shift, e)) continue;
         rice_cfg rc;
         memset(&rc, 0, sizeof(rc));

@@ -149,6 +149,8 @@ int oracle_lpc_levinson(const int64_t *R, unsigned max_order, double *coefs);
 int oracle_lpc_levinson_err(const int64_t *R, unsigned max_order, double *coefs, double *errs);
 double oracle_lpc_order_key(double err, unsigned q, uint32_t n, unsigned bps);
 int oracle_lpc_quantize(const double *a, unsigned order, unsigned precision, int32_t *q, int *shift);
+/* analysis mode (not the contract): exhaustive LPC order search, for compression comparisons */
+void oracle_set_lpc_exhaustive(int on);
 
 /* Exposed pieces for unit tests. */
 uint64_t oracle_rice_part_size(uint64_t len, uint32_t param, uint64_t abs_sum);

@@ -241,3 +241,24 @@ def test_lpc_selects_the_order_of_the_smallest_key():
     keys = [(_py_key(errs[q - 1], q, n, bps), q) for q in range(1, len(errs) + 1)
             if _py_quantize(coefs[q - 1]) is not None]
     assert sub.order == min(keys)[1]
+
+
+def test_exhaustive_order_search_analysis_mode():
+    """tools/lpc_ratio.py's analysis mode (oracle_set_lpc_exhaustive; NOT the contract the GPU
+    implements): every order's Rice search, smallest total kept -- lossless, never larger than the
+    contract's single order, and switched off again the default encode is the contract's."""
+    import oracle_ref
+    import synth
+
+    L = oracle_ref.lib()
+    pcm = synth.synth_pcm(4096 * 6 + 77, 2, 24, 96000, stream=9)
+    base, _, _ = oracle_ref.encode_stream(pcm, 2, 24, 96000, lpc=8)
+    L.oracle_set_lpc_exhaustive(1)
+    try:
+        exh, _, _ = oracle_ref.encode_stream(pcm, 2, 24, 96000, lpc=8)
+    finally:
+        L.oracle_set_lpc_exhaustive(0)
+    assert len(exh) <= len(base)
+    dec, _ = oracle_ref.decode_frames(exh, 2, 24, 96000, len(pcm) // 6)
+    assert dec == pcm
+    assert oracle_ref.encode_stream(pcm, 2, 24, 96000, lpc=8)[0] == base
