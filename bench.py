@@ -1346,6 +1346,8 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
     if s:
         line["sharded_stream"] = {"value": s.get("value"), "ranks": s.get("ranks"), "ms_per_window": s.get("ms_per_window"),
                                   "output_ok": s.get("output_ok")}
+        if s.get("error"):
+            line["sharded_stream"]["error"] = s["error"]
     line["detail"] = detail_path
     # last resort, never expected: drop the largest optional blocks until the line fits
     for k in ("stream_curve", "end_to_end", "kernel_ms_per_step", "configs"):
@@ -1527,7 +1529,13 @@ def main():
     if not args.no_sharded:
         del d_pcm
         torch.cuda.empty_cache()
-        sharded = sharded_stream(args, rank, world, dist, dev)
+        try:
+            sharded = sharded_stream(args, rank, world, dist, dev)
+        except Exception as e:
+            # the C ABI agrees on errors across ranks (every rank raises alike), so the headline
+            # measured above still reaches the line; the failure is reported in it
+            print(f"bench.py: sharded stream failed: {e!r}", file=sys.stderr)
+            sharded = {"error": f"{type(e).__name__}: {e}"[:300], "output_ok": False, "ranks": world}
         d_pcm = torch.from_numpy(buf).to(dev) if (rank == 0 and world == 1 and not args.no_curve
                                                   and not args.no_md5) else None
 

@@ -87,6 +87,24 @@ def test_sharded_gpu_rccl_device_gather(tmp_path, nproc, n):
     assert out == oracle_ref.encode_file(pcm, 2, 16, 44100)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,ch,bits", [("gather", 2, 16), ("capi", 2, 16), ("capi", 8, 24), ("windows", 2, 16)])
+def test_comm_self_p2p_one_rank(tmp_path, monkeypatch, mode, ch, bits):
+    """FLACGPU_COMM_SELF_P2P=1: rank 0 moves its own slice into the receive buffer by RCCL
+    send/recv to itself instead of a device copy, so the grouped ncclSend / ncclRecv code that the
+    other ranks' slices take (fg_comm.cpp transfer) runs on the one-GPU box: the count exchange of
+    parallel.gather_comm, flacgpu_encode_frames_sharded's windows (max_frames 4: 11 gathers), and
+    ShardedStream (frames in place, sizes by send/recv).  Same file as the restatement's."""
+    monkeypatch.setenv("FLACGPU_COMM_SELF_P2P", "1")
+    n = 40 * 4096 + 777 if mode != "windows" else 3 * 5 * 4096
+    extra = {"gather": ["--gather", "capi"], "capi": ["--mode", "capi", "--max-frames", "4"],
+             "windows": ["--mode", "windows", "--windows", "3", "--frames-per-rank", "5"]}[mode]
+    out = run_workers(tmp_path, 1, "--encoder", "gpu", "--backend", "nccl", "--channels", str(ch), "--bits",
+                      str(bits), "--samples", str(n), *extra)
+    pcm = synth.synth_pcm(n, ch, bits, 44100)
+    assert out == oracle_ref.encode_file(pcm, ch, bits, 44100)
+
+
 @pytest.mark.parametrize("nproc,ch,bits,windows,f", [(2, 2, 16, 3, 2), (2, 8, 24, 2, 1), (3, 1, 16, 2, 3)])
 def test_sharded_stream_windows_gloo(tmp_path, nproc, ch, bits, windows, f):
     """parallel.ShardedStream (the bench's sharded-stream mode) on world_size > 1 with gloo:

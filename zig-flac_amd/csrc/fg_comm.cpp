@@ -93,6 +93,10 @@ struct flacgpu_comm {
     uint8_t *d_recv = nullptr;
     uint32_t *d_recv_sizes = nullptr;
     uint64_t recv_cap = 0, recv_sizes_cap = 0;
+    // FLACGPU_COMM_SELF_P2P=1 (read at init; output-invariant): rank 0 moves its own slice into the
+    // receive buffer by RCCL send/recv to itself instead of a device copy, so that a one-GPU box runs
+    // the grouped point-to-point code the other ranks' slices take
+    bool self_p2p = false;
 };
 
 namespace {
@@ -132,14 +136,24 @@ int transfer(flacgpu_comm *m, const uint8_t *d_frames, const uint32_t *d_sizes, 
     }
     const uint64_t my_b = all[m->rank * kWords + kBytes], my_f = all[m->rank * kWords + kFrames];
     if (m->rank == 0) {
-        if (my_b && d_frames != d_recv)
-            CHK_HIP(hipMemcpyAsync(d_recv, d_frames, my_b, hipMemcpyDeviceToDevice, st));
-        if (my_f && d_sizes != d_recv_sizes)
+        // its own slice: in place, a device copy, or (self_p2p) send/recv to itself
+        const bool pb = my_b && d_frames != d_recv, pf = my_f && d_sizes != d_recv_sizes;
+        if (pb && !m->self_p2p) CHK_HIP(hipMemcpyAsync(d_recv, d_frames, my_b, hipMemcpyDeviceToDevice, st));
+        if (pf && !m->self_p2p)
             CHK_HIP(hipMemcpyAsync(d_recv_sizes, d_sizes, my_f * 4, hipMemcpyDeviceToDevice, st));
-        if (m->world == 1) return FLACGPU_OK;
+        const bool self = m->self_p2p && (pb || pf);
+        if (m->world == 1 && !self) return FLACGPU_OK;
         CHK_NCCL(r.group_start());
         uint64_t ob = my_b, of = my_f;
         bool bad = false;
+        if (self && pf) {
+            bad |= r.recv(d_recv_sizes, my_f, ncclUint32, 0, m->nc, st) != ncclSuccess;
+            bad |= r.send(d_sizes, my_f, ncclUint32, 0, m->nc, st) != ncclSuccess;
+        }
+        if (self && pb) {
+            bad |= r.recv(d_recv, my_b, ncclUint8, 0, m->nc, st) != ncclSuccess;
+            bad |= r.send(d_frames, my_b, ncclUint8, 0, m->nc, st) != ncclSuccess;
+        }
         for (int k = 1; k < m->world; k++) {
             const uint64_t nb = all[k * kWords + kBytes], nf = all[k * kWords + kFrames];
             if (nf) bad |= r.recv(d_recv_sizes + of, nf, ncclUint32, k, m->nc, st) != ncclSuccess;
@@ -187,6 +201,7 @@ int flacgpu_comm_init(const uint8_t id[FLACGPU_COMM_ID_BYTES], int world, int ra
     m->world = world;
     m->rank = rank;
     m->device = device;
+    if (const char *e = std::getenv("FLACGPU_COMM_SELF_P2P")) m->self_p2p = std::atoi(e) != 0;
     auto fail = [&](int rc) {
         flacgpu_comm_destroy(m);
         return rc;
