@@ -1342,6 +1342,8 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
                                              if e.get("many_files") else None),
                               "vs_cpu_single_socket_estimate": e.get("vs_cpu_single_socket_estimate"),
                               "output_ok": e.get("output_ok")}
+        if e.get("error"):
+            line["end_to_end"]["error"] = e["error"]
     s = full.get("sharded_stream")
     if s:
         line["sharded_stream"] = {"value": s.get("value"), "ranks": s.get("ranks"), "ms_per_window": s.get("ms_per_window"),
@@ -1544,7 +1546,11 @@ def main():
         del d_pcm
         d_pcm = None
         torch.cuda.empty_cache()
-        e2e = end_to_end_node(args, rank, world, dist, dev)
+        try:
+            e2e = end_to_end_node(args, rank, world, dist, dev)
+        except Exception as e:  # as the sharded leg: the headline still reaches the line
+            print(f"bench.py: end-to-end (node) failed: {e!r}", file=sys.stderr)
+            e2e = {"error": f"{type(e).__name__}: {e}"[:300], "output_ok": False, "ranks": world}
     if rank == 0 and world == 1:
         if not args.no_curve and not args.no_md5:
             curve = stream_curve(args, enc, d_pcm, buf, fb, dev)

@@ -59,6 +59,18 @@ def test_compact_line_round6_keys():
         assert "frac_vs_6p29" in v and "cpu_health" in v
 
 
+def test_compact_line_reports_a_failed_multi_rank_leg():
+    """A sharded or node end-to-end leg that raised on every rank leaves the headline in the line,
+    its failure named beside it (bench.py main)."""
+    full = _full()
+    full["sharded_stream"] = {"error": "FlacGpuError: comm_init", "output_ok": False, "ranks": 8}
+    full["end_to_end"] = {"error": "RuntimeError: x", "output_ok": False, "ranks": 8}
+    line = bench.compact_line(full, "x")
+    assert line["value"] == full["value"] and len(json.dumps(line)) <= bench.LINE_MAX
+    assert line["sharded_stream"]["error"].startswith("FlacGpuError") and line["sharded_stream"]["output_ok"] is False
+    assert line["end_to_end"]["error"] == "RuntimeError: x" and line["end_to_end"]["ranks"] == 8
+
+
 def test_cpu_pick_cores_one_per_physical_core():
     cpus, info = bench.pick_cores(2, "idle")
     assert len(cpus) == len(set(cpus)) <= 2

@@ -56,12 +56,15 @@ def test_sharded_gather_gloo_matches_whole_file(tmp_path, nproc, ch, bits, n):
 
 
 @pytest.mark.gpu
-def test_sharded_gpu_two_ranks_one_device(tmp_path):
-    """GPU frames stay in device memory; the gather moves CPU tensors under gloo."""
-    n = 12 * 4096 + 999
-    out = run_workers(tmp_path, 2, "--encoder", "gpu", "--samples", str(n), "--md5", "gpu")
-    pcm = synth.synth_pcm(n, 2, 16, 44100)
-    assert out == oracle_ref.encode_file(pcm, 2, 16, 44100)
+@pytest.mark.parametrize("nproc,ch,bits,n,md5", [(2, 2, 16, 12 * 4096 + 999, "gpu"), (3, 8, 24, 7 * 4096 + 5, "host"),
+                                                 (4, 1, 32, 9 * 4096, "host"), (3, 2, 16, 2 * 4096 + 1, "gpu")])
+def test_sharded_gpu_ranks_one_device(tmp_path, nproc, ch, bits, n, md5):
+    """The GPU encoder on every rank (ranks share the one device), the gather over gloo (CPU
+    tensors): uneven frame ranges, a rank with one frame, 24-bit 8-channel and 32-bit mono."""
+    out = run_workers(tmp_path, nproc, "--encoder", "gpu", "--channels", str(ch), "--bits", str(bits), "--samples",
+                      str(n), "--md5", md5)
+    pcm = synth.synth_pcm(n, ch, bits, 44100)
+    assert out == oracle_ref.encode_file(pcm, ch, bits, 44100)
 
 
 def _gpus():
