@@ -1192,6 +1192,12 @@ def workload_text(args, F):
             (", MD5 off (diagnostic)" if args.no_md5 else ", MD5 on its own HIP stream beside the next step's encode"))
 
 
+def rate_units(value, channels, rate):
+    """SURVEY §8(d)'s companions of the interchannel-sample metric: channel samples per second and
+    the multiple of real time (seconds of audio encoded per second) for the same throughput."""
+    return {"channel_msamples_per_s": round(value * channels, 1), "x_realtime": round(value * 1e6 / rate, 1)}
+
+
 def config_line(args, cfg, dist, rank, world, dev, cpu=None):
     """One BASELINE config (c3 / c4 / c5) as its own timed line inside the default run: its preset,
     65536-block steps, barrier + max over ranks, output compared with the oracle after timing, the
@@ -1236,6 +1242,7 @@ def config_line(args, cfg, dist, rank, world, dev, cpu=None):
                 "compression_ratio": round(out_bytes / pcm_bytes, 4),
                 "roofline": roofline_of(sub, kt, args.cfg_steps, pcm_bytes, out_bytes, ms, workload_key(sub)),
                 "output_ok": ok, "verified": vinfo, "cpu_baseline": None}
+        line["units"] = rate_units(line["value"], sub.channels, sub.rate)
         if cpu:  # measured before torch (main(), cpu_legs)
             line["cpu_baseline"] = cpu
             line["vs_cpu_single_socket_estimate"] = (round(line["value"] / line["cpu_baseline"]["single_socket_estimate"], 1)
@@ -1296,7 +1303,7 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
     roofline and CPU baseline, one summary per BASELINE config and one-number summaries of the
     stream curve, the end-to-end path and the sharded stream.  len(json.dumps(...)) <= LINE_MAX
     (tests/test_bench_line.py); everything else is in the sidecar named by `detail`."""
-    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+    keep = ("metric", "value", "unit", "units", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
             "vs_baseline", "dtype", "data")
     line = {k: full.get(k) for k in keep}
     cfg = full.get("config") or {}
@@ -1319,6 +1326,7 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
                            "step_issue_frac": r.get("step_issue_frac"),
                            "weighted_issue_frac": r.get("weighted_issue_frac"),
                            "traffic_ratio": (r.get("kernels") or {}).get(_dom_name(r), {}).get("traffic_ratio"),
+                           "x_realtime": (c.get("units") or {}).get("x_realtime"),
                            "output_ok": c.get("output_ok"), "cpu": cb.get("value"),
                            "cpu_single_core": (cb.get("single_core") or {}).get("value"),
                            "cpu_health": cb.get("health")}
@@ -1580,6 +1588,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "MSamples/s",
+            "units": rate_units(value, args.channels, args.rate),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,

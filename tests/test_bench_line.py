@@ -59,6 +59,20 @@ def test_compact_line_round6_keys():
         assert "frac_vs_6p29" in v and "cpu_health" in v
 
 
+def test_rate_units_and_line_keys():
+    """channel-samples/s and x-realtime beside the interchannel MSamples/s."""
+    u = bench.rate_units(153000.0, 2, 44100)
+    assert u == {"channel_msamples_per_s": 306000.0, "x_realtime": round(153000e6 / 44100, 1)}
+    full = _full()
+    full["units"] = u
+    for c in full.get("configs") or []:
+        c["units"] = bench.rate_units(c["value"], 2, 96000)
+    line = bench.compact_line(full, "x")
+    assert line["units"] == u and len(json.dumps(line)) <= bench.LINE_MAX
+    for v in line["configs"].values():
+        assert v["x_realtime"] > 0
+
+
 def test_compact_line_reports_a_failed_multi_rank_leg():
     """A sharded or node end-to-end leg that raised on every rank leaves the headline in the line,
     its failure named beside it (bench.py main)."""
