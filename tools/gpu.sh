@@ -21,6 +21,9 @@
 #                                                          overlapped schedule) against build_diag/libflacgpu.so
 #   tools/gpu.sh e2e <tag> <threads...>                    tools/e2e_probe.py once per host MD5 pool size
 #                                                          -> gpurun_out/<tag>_e2e_<threads>.json
+#   tools/gpu.sh e2etrace <tag>                            rocprofv3 kernel + memory-copy trace of one e2e probe
+#                                                          (env E2E_FILES 64, E2E_MANY 0, E2E_THREADS 16) ->
+#                                                          tools/overlap.py -> gpurun_out/<tag>_e2e_overlap.json
 #   tools/gpu.sh cpuplace <tag>                            CPU-baseline legs alone (no GPU) under each thread
 #                                                          placement -> gpurun_out/<tag>_cpu_<place>.json
 #   tools/gpu.sh final  <tag>                              tests + smoke + profiles of every config at
@@ -142,6 +145,17 @@ do_e2e() {
   done
 }
 
+do_e2etrace() {  # rocprofv3 kernel + memory-copy trace (no counters) of one end-to-end probe -> overlap summary
+  local OUT=$REPO/gpurun_out/e2etrace_$TAG
+  mkdir -p $OUT
+  (cd /tmp && export TMPDIR=/tmp && FLACGPU_MD5_THREADS=${E2E_THREADS:-16} timeout -k 10 400 rocprofv3 --kernel-trace \
+     --memory-copy-trace --output-format csv -d $OUT/tr -o tr -- python3 $REPO/tools/e2e_probe.py \
+     --e2e-files ${E2E_FILES:-64} --e2e-many ${E2E_MANY:-0} $E2E_ARGS > $OUT/tr.log 2>&1) ||
+    { echo "trace failed"; tail -5 $OUT/tr.log; return 1; }
+  tail -1 $OUT/tr.log
+  python3 tools/overlap.py $OUT/tr gpurun_out/${TAG}_e2e_overlap.json > /dev/null
+}
+
 do_cpuplace() {
   for place in socket0 idle none; do
     timeout -k 10 300 python -u bench.py --cpu-only --cpu-place $place --configs=c5 > gpurun_out/${TAG}_cpu_$place.json 2> gpurun_out/${TAG}_cpu_$place.err ||
@@ -163,6 +177,7 @@ case $CMD in
   stamps) do_stamps ;;
   cpuplace) do_cpuplace ;;
   e2e) do_e2e "$@" ;;
+  e2etrace) do_e2etrace ;;
   diagtests) do_diagtests ;;
   final)
     do_tests && do_smoke &&
