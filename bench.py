@@ -118,7 +118,8 @@ def parse():
                         "are allocated (pinned pages and the MD5 pool's reads on the GPU's side of the fabric)")
     p.add_argument("--no-sharded", action="store_true", help="skip the sharded single-stream line")
     p.add_argument("--sharded-config", choices=sorted(PRESETS), default="c4")
-    p.add_argument("--sharded-frames", type=int, default=8192, help="frames per rank per window (sharded mode)")
+    p.add_argument("--sharded-frames", type=int, default=32768,
+                   help="frames per rank per window (sharded mode; SURVEY 8(d): 32768 blocks per GPU for C4)")
     p.add_argument("--sharded-steps", type=int, default=10)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-frames", type=int, default=32768, help="blocks of the CPU-baseline input (cycled)")
