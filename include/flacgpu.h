@@ -135,7 +135,8 @@ int flacgpu_multi_encode_frames(flacgpu_multi *m, const void *pcm, uint32_t byte
  * librccl.so.1 is loaded on first use (an RCCL already in the process, e.g. a
  * framework's, is reused; else /opt/rocm/lib); without it these return
  * FLACGPU_ERR_DEVICE.  Every call below is collective: every rank of the
- * communicator makes it, in the same order. */
+ * communicator makes it, in the same order.  A communicator is used by one host
+ * thread at a time (as a flacgpu_ctx is): its count buffers are per communicator. */
 typedef struct flacgpu_comm flacgpu_comm;
 #define FLACGPU_COMM_ID_BYTES 128
 /* Rank 0 creates the communicator id; the host hands it to every rank (a file,
